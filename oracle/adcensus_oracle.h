@@ -1,0 +1,124 @@
+/*
+ * adcensus_oracle.h -- CPU restatement of the reference AD-Census path.
+ *
+ * TEST INFRASTRUCTURE ONLY.  This library is the parity checker for the HIP
+ * product path (tea_stereo_matching_amd/csrc).  Only tests/, __graft_entry__.smoke()
+ * and bench.py's cpu_baseline leg may load it.  The product never links it.
+ *
+ * Reference: YYpasser/tea_stereo_matching, source/ADCensus.cpp (stereo::ADCensus),
+ * include/stereo_utils.h:191-244 + source/stereo_utils.cpp:271-326 (ADCensusParams).
+ * Every function in adcensus_oracle.c cites the reference line range it restates.
+ *
+ * Parity pinning: the reference needs OpenCV 4.13 (absent from this image), so it
+ * is unbuildable here and cannot be run.  The oracle is pinned against the only
+ * output fixtures the reference ships (demo-output/0600_adcensus.png and
+ * 0045_ADCensus.png, JET-colourised disparity maps); see DESIGN.md "Oracle".
+ * The four OpenCV calls on the path (equalizeHist, blur, Canny, medianBlur) are
+ * restated from OpenCV 4.x semantics in cvops.c -- parity unpinned at that boundary
+ * beyond what the demo fixtures show.
+ *
+ * Layouts follow the reference: cost volumes [view][d][H][W] fp32 (ADCensus.cpp:289),
+ * arm maps [view][dir][H][W] int32 with dir = up, down, left, right (ADCensus.cpp:762-765),
+ * images BGR u8 interleaved with a row stride in bytes (cv::Mat CV_8UC3).
+ */
+#ifndef TSM_ADCENSUS_ORACLE_H
+#define TSM_ADCENSUS_ORACLE_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+enum { ORC_RGB = 0, ORC_HSI = 1 };
+enum { ORC_CENSUSWIN_9x7 = 0, ORC_CENSUSWIN_7x5 = 1 };
+
+/* Mirrors stereo::ADCensusParams (stereo_utils.h:209-244) plus ADCensusImpl state
+ * (ADCensus.cpp:276-295). */
+typedef struct orc_params {
+    int color_model;        /* ColorModel (stereo_utils.h:191-195) */
+    int roi_matching;       /* m_roiMatching */
+    int mask_matching;      /* m_maskMatching */
+    int offset;             /* m_offset */
+    int min_disparity;      /* m_minDisparity */
+    int max_disparity;      /* m_maxDisparity (inclusive: L = max-min+1) */
+    float lambda_ad;
+    int census_win;
+    float lambda_census;
+    float lambda_hue, lambda_saturation, lambda_intensity;
+    int color_thresh1, color_thresh2;
+    int saturation_thresh1, saturation_thresh2;
+    int intensity_thresh1, intensity_thresh2;
+    int max_length1, max_length2;
+    int iterations;
+    int color_diff;
+    float pi1, pi2;
+    int disp_tolerance;
+    int voting_thresh;
+    float voting_ratio_thresh;
+    int max_search_depth;
+    int blur_kernel_size;
+    int canny_thresh1, canny_thresh2, canny_kernel_size;
+    /* --- oracle execution controls (not reference state) --- */
+    int num_threads;        /* OpenMP threads for the pure stages; 0 = runtime default */
+    int scan_emulate_threads; /* 0/1: serial scanline semantics (deterministic intent).
+                                 T>1: emulate the reference's racy omp-static schedule
+                                 (ADCensus.cpp:801-853): the first row/col of each of the
+                                 T chunks reads its predecessor's pre-pass value. */
+} orc_params;
+
+/* ADCensusImpl() defaults (ADCensus.cpp:409-420) + setADCensusParams (stereo_utils.cpp:271-326). */
+void orc_default_params(orc_params* p, int color_model);
+
+/* Optional per-stage dumps (all in reference layout; NULL = skip). */
+typedef struct orc_dump {
+    uint8_t* images;       /* [2][H][W][3] images actually matched (HSI-converted in HSI mode) */
+    float* cost_init;      /* [2][L][H][W] after costInitialize */
+    int32_t* arms;         /* [2][4][H][W] up, down, left, right */
+    float* cost_agg;       /* [2][L][H][W] after costAggregate */
+    float* cost_scan;      /* [2][L][H][W] after scanlineOptimize */
+    int32_t* wta;          /* [2][H][W] cost2disparity(0), (1) */
+    int32_t* outlier;      /* [H][W] outlierElimination */
+    int32_t* voting;       /* [H][W] after the 5 regionVoting calls */
+    int32_t* interp;       /* [H][W] after properInterpolation */
+    uint8_t* gray;         /* [H][W] convertDisp2Gray (after equalizeHist) */
+    uint8_t* edges;        /* [H][W] Canny output (0/255) */
+    int32_t* adjusted;     /* [H][W] after discontinuityAdjustment */
+    float* subpix;         /* [H][W] subpixel map before medianBlur */
+} orc_dump;
+
+/* ADCensus::compute (ADCensus.cpp:330-407).  left/right: BGR u8, `step` bytes per row.
+ * out: H*W floats (row-major, dense).  Returns 0 or a negative error code:
+ *   -1 image error (empty / size mismatch), -2 bad disparity range, -3 internal. */
+int orc_compute(const orc_params* p, const uint8_t* left, const uint8_t* right,
+                int rows, int cols, size_t step, float* out, orc_dump* dump);
+
+/* Validation helpers mirroring the reference setters (ADCensus.cpp:307-328). */
+int orc_check_disparity_range(int min_disparity, int max_disparity); /* 0 ok, -2 error */
+
+/* Pure per-stage entry points (for fine-grained tests). */
+void orc_cost_initialize(const orc_params* p, const uint8_t* img0, const uint8_t* img1,
+                         int H, int W, float* vol /*[2][L][H][W]*/);
+void orc_compute_limits(const orc_params* p, const uint8_t* img0, const uint8_t* img1,
+                        int H, int W, int32_t* arms /*[2][4][H][W]*/);
+void orc_cost_aggregate(const orc_params* p, int H, int W, const int32_t* arms, float* vol);
+void orc_scanline_optimize(const orc_params* p, const uint8_t* img0, const uint8_t* img1,
+                           int H, int W, float* vol);
+void orc_cost2disparity(const orc_params* p, int H, int W, const float* vol_view, int32_t* disp);
+
+/* OpenCV 4.x restatements (cvops.c). */
+void orc_cv_equalize_hist(const uint8_t* src, uint8_t* dst, int H, int W);
+void orc_cv_blur3(const uint8_t* src, uint8_t* dst, int H, int W);           /* boxFilter 3x3, REFLECT_101 */
+void orc_cv_canny(const uint8_t* src, uint8_t* dst, int H, int W, double low, double high); /* aperture 3, L1 */
+void orc_cv_median3f(const float* src, float* dst, int H, int W);            /* medianBlur 3, CV_32F */
+void orc_cv_gauss3_filter2d(const uint8_t* src, uint8_t* dst, int H, int W); /* filter2D 3x3 gaussian (sigma<=0), BORDER_CONSTANT, 3 channels */
+
+/* JET colour map (stereo.cpp:75-92) and applyColorMap min/max (stereo.cpp:94-118). */
+void orc_jet_colormap(uint8_t lut[256][3]);
+void orc_apply_colormap(const float* disp, int H, int W, uint8_t* bgr_out);
+
+#ifdef __cplusplus
+}
+#endif
+#endif
