@@ -1,0 +1,42 @@
+# Builds the MI355X (gfx950) AD-Census library and the CPU oracle.
+#   make            -> tea_stereo_matching_amd/lib/libtsm_adcensus.so + oracle/build/liboracle_adcensus.so
+#   make -j16 lib   -> library only
+# -ffp-contract=off: hipcc contracts a*b+c into FMA by default, which would break
+# bit-exactness with the reference's uncontracted float expressions.
+HIPCC    ?= /opt/rocm/bin/hipcc
+ARCH     ?= gfx950
+SRC      := tea_stereo_matching_amd/csrc
+OBJ      := build/obj
+LIBDIR   := tea_stereo_matching_amd/lib
+LIB      := $(LIBDIR)/libtsm_adcensus.so
+HIPFLAGS := --offload-arch=$(ARCH) -O3 -std=c++20 -fPIC -ffp-contract=off \
+            -fhip-fp32-correctly-rounded-divide-sqrt -Wall -Wno-unused-result -Wno-unused-value -Iinclude
+HIP_SRCS := k_cost k_aggregate k_scanline k_refine
+CPP_SRCS := engine stereo_api
+OBJS     := $(addprefix $(OBJ)/,$(addsuffix .o,$(HIP_SRCS) $(CPP_SRCS)))
+HDRS     := $(SRC)/tsm_device.h $(SRC)/tsm_launch.h include/tsm_adcensus.h include/stereo.h
+
+all: lib oracle
+
+lib: $(LIB)
+
+$(OBJ)/%.o: $(SRC)/%.hip $(HDRS)
+	@mkdir -p $(OBJ)
+	$(HIPCC) $(HIPFLAGS) -c $< -o $@
+
+$(OBJ)/%.o: $(SRC)/%.cpp $(HDRS)
+	@mkdir -p $(OBJ)
+	$(HIPCC) $(HIPFLAGS) -c $< -o $@
+
+$(LIB): $(OBJS)
+	@mkdir -p $(LIBDIR)
+	$(HIPCC) --offload-arch=$(ARCH) -shared -o $@ $(OBJS)
+
+oracle:
+	$(MAKE) -C oracle
+
+clean:
+	rm -rf build $(LIBDIR)
+	$(MAKE) -C oracle clean
+
+.PHONY: all lib oracle clean

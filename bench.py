@@ -1,0 +1,206 @@
+#!/usr/bin/env python3
+"""Benchmark: AD-Census stereo pairs/s on MI355X (BASELINE.json metric).
+
+Workload (configs[1]): synthetic KITTI-shape 1242x375 BGR pairs,
+setMinMaxDisparity(0, 192) (193 labels), RGB, the FULL pipeline (cost volume,
+4x cross aggregation, 4-direction scanline, WTA/LR check, 5x voting, interpolation,
+discontinuity adjustment, subpixel + median).  One step = every rank computes its
+batch of `--batch` pairs (inputs already resident in HBM) and rank 0 gathers the
+disparity maps over RCCL.  Weak scaling: per-GPU work is fixed as N grows.
+
+  python bench.py [--gpus N --steps K --warmup W]
+  python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N ...
+
+Rank 0 prints ONE JSON line.  `roofline` prices the dominant kernel named by
+BASELINE.json (the cost-volume build) from HIP events around it on its own stream;
+`cpu_baseline` times the oracle (the C restatement of the reference's OpenMP path)
+on one pair on this host's cores.
+"""
+from __future__ import annotations
+
+import argparse
+import glob
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E peak (MI355X_MICROARCH.md chip table)
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--batch", type=int, default=8, help="pairs per GPU per step")
+    ap.add_argument("--concurrency", type=int, default=2, help="pair pipelines in flight per GPU")
+    ap.add_argument("--height", type=int, default=375)
+    ap.add_argument("--width", type=int, default=1242)
+    ap.add_argument("--max-disparity", type=int, default=192)
+    ap.add_argument("--no-gather", action="store_true")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-threads", type=int, default=0)
+    return ap.parse_args()
+
+
+def cpu_baseline(args, left, right):
+    """Oracle (`port` of the reference path, same per-(p,d) census and OpenMP
+    decomposition) on one pair on this host: ~10-30 s of CPU work."""
+    from oracle import oracle as O
+
+    threads = args.cpu_threads or min(16, os.cpu_count() or 1)
+    p = O.default_params(O.RGB, 0, args.max_disparity, num_threads=threads)
+    t0 = time.perf_counter()
+    O.compute(left, right, p)
+    dt = time.perf_counter() - t0
+    return {"value": 1.0 / dt, "unit": "pairs/s", "cores": threads, "kind": "port",
+            "sample": f"1 synthetic pair (seed 1000) {args.width}x{args.height} D=[0,{args.max_disparity}] "
+                      f"RGB, oracle/ C restatement with OpenMP, {dt:.2f} s/pair"}
+
+
+def pmc_traffic():
+    """HBM bytes per cost-volume launch from the committed rocprofv3 --pmc summary
+    (profiles/*cost_pmc*.json, FETCH_SIZE doubled per the gfx950 rule), else None."""
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*cost_pmc*.json")))
+    if not files:
+        return None
+    try:
+        with open(files[-1]) as f:
+            return json.load(f).get("hbm_bytes_per_launch")
+    except Exception:
+        return None
+
+
+def main():
+    args = parse()
+    import numpy as np
+    import torch
+    import torch.distributed as dist
+
+    import tea_stereo_matching_amd as tsm
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    dev = torch.device("cuda", local)
+    torch.cuda.set_device(dev)
+
+    H, W, D = args.height, args.width, args.max_disparity
+    L = D + 1
+    B = args.batch
+    # synthetic inputs: pair i of rank r uses seed 1000 + r*B + i; uploaded once (HBM-resident)
+    lefts, rights = [], []
+    for i in range(B):
+        l, r, _ = tsm.synthetic.make_scene(1000 + rank * B + i, H, W, L)
+        lefts.append(torch.from_numpy(l).to(dev))
+        rights.append(torch.from_numpy(r).to(dev))
+    outs = torch.empty((B, H, W), dtype=torch.float32, device=dev)
+    torch.cuda.synchronize()
+
+    m = tsm.ADCensus(local)
+    m.setMatchingStrategy(tsm.ColorModel.RGB, False, False)
+    m.setMinMaxDisparity(0, D)
+    m.setConcurrency(args.concurrency)
+    lp = [t.data_ptr() for t in lefts]
+    rp = [t.data_ptr() for t in rights]
+    op = [outs[i].data_ptr() for i in range(B)]
+    gathered = None
+    if rank == 0 and world > 1 and not args.no_gather:
+        gathered = [torch.empty_like(outs) for _ in range(world)]
+
+    def step():
+        m.compute_batch_device_ptr(lp, rp, H, W, W * 3, op, W * 4)
+        if world > 1 and not args.no_gather:
+            dist.gather(outs, gathered if rank == 0 else None, dst=0)
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    m.setProfiling(True)
+    m.resetStageTimes()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    m.setProfiling(False)
+    stages = m.stageTimes()
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+
+    pairs = world * B * args.steps
+    value = pairs / elapsed
+    N = H * W
+    # algorithmic bytes of one cost-volume launch (both views, one pair):
+    #   4*L*N*V (fp32 volume writes, V=2 views) + 2*3*N (two BGR images read)
+    b_build = 4 * L * N * 2 + 2 * 3 * N
+    cost_ms, cost_n = stages["cost"]
+    t_cost = cost_ms / max(1, cost_n) / 1e3
+    achieved = b_build / t_cost / 1e9 if t_cost > 0 else None
+    traffic = pmc_traffic()
+    stage_ms = {k: round(v[0] / max(1, v[1]), 4) for k, v in stages.items()}
+
+    line = {
+        "metric": "stereo pairs/s, 1242x375 D=192 (193 labels), full AD-Census pipeline",
+        "value": round(value, 3),
+        "unit": "pairs/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(elapsed / args.steps * 1e3, 3),
+        "ms_per_frame": round(elapsed / (B * args.steps) * 1e3, 4),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "f32",
+        "data": "synthetic (splitmix64 layered scenes, SURVEY §8d), inputs resident in HBM",
+        "config": {
+            "workload": f"config B: {W}x{H} BGR, setMinMaxDisparity(0,{D}), RGB, full pipeline",
+            "pairs_per_gpu_per_step": B,
+            "global_batch": world * B,
+            "concurrency": args.concurrency,
+            "parallelism": f"dp{world} (pairs sharded, RCCL gather to rank 0)" if world > 1 else "dp1",
+            "gather": world > 1 and not args.no_gather,
+        },
+        "stage_ms_per_pair": stage_ms,
+        "roofline": {
+            "kernel": "k_cost_volume (costInitialize, ADCensus.cpp:522-581)",
+            "bound": "hbm",
+            "achieved": round(achieved, 1) if achieved else None,
+            "peak": HBM_PEAK_GBS,
+            "unit": "GB/s",
+            "frac": round(achieved / HBM_PEAK_GBS, 4) if achieved else None,
+            "traffic": traffic,
+            "algorithmic_bytes_per_launch": b_build,
+            "avg_launch_ms": round(t_cost * 1e3, 4),
+        },
+    }
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        l, r, _ = tsm.synthetic.make_scene(1000, H, W, L)
+        line["cpu_baseline"] = cpu_baseline(args, l, r)
+        line["speedup_vs_cpu_baseline"] = round(value / line["cpu_baseline"]["value"], 1)
+    else:
+        line["cpu_baseline"] = None
+    m.close()
+    if rank == 0:
+        print(json.dumps(line), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

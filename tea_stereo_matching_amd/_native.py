@@ -1,0 +1,116 @@
+"""Loader for the gfx950 AD-Census library (libtsm_adcensus.so) and its C ABI.
+
+The library is built in-tree (``make lib`` / ``__graft_entry__.build()``).  There is no
+fallback: if the shared object is missing, importing the bindings raises.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "lib", "libtsm_adcensus.so")
+HEADER_PATH = os.path.join(os.path.dirname(_HERE), "include", "tsm_adcensus.h")
+
+TSM_OK = 0
+TSM_ERR_ARGUMENT = -1
+TSM_ERR_DISPARITY_RANGE = -2
+TSM_ERR_OFFSET = -3
+TSM_ERR_IMAGE = -4
+TSM_ERR_DEVICE = -5
+TSM_ERR_OUT_OF_MEMORY = -6
+TSM_ERR_UNSUPPORTED = -7
+
+STAGES = ("prep", "cost", "arms", "aggregate", "scanline", "refine")
+
+_P = ctypes.c_void_p
+
+
+class TsmParams(ctypes.Structure):
+    """tsm_adc_params (mirrors stereo::ADCensusParams, stereo_utils.h:209-244)."""
+
+    _fields_ = [
+        ("lambda_ad", ctypes.c_float), ("census_win", ctypes.c_int),
+        ("lambda_census", ctypes.c_float), ("lambda_hue", ctypes.c_float),
+        ("lambda_saturation", ctypes.c_float), ("lambda_intensity", ctypes.c_float),
+        ("color_thresh1", ctypes.c_int), ("color_thresh2", ctypes.c_int),
+        ("saturation_thresh1", ctypes.c_int), ("saturation_thresh2", ctypes.c_int),
+        ("intensity_thresh1", ctypes.c_int), ("intensity_thresh2", ctypes.c_int),
+        ("max_length1", ctypes.c_int), ("max_length2", ctypes.c_int),
+        ("iterations", ctypes.c_int), ("color_diff", ctypes.c_int),
+        ("pi1", ctypes.c_float), ("pi2", ctypes.c_float),
+        ("disp_tolerance", ctypes.c_int), ("voting_thresh", ctypes.c_int),
+        ("voting_ratio_thresh", ctypes.c_float), ("max_search_depth", ctypes.c_int),
+        ("blur_kernel_size", ctypes.c_int), ("canny_thresh1", ctypes.c_int),
+        ("canny_thresh2", ctypes.c_int), ("canny_kernel_size", ctypes.c_int),
+    ]
+
+
+class TsmDump(ctypes.Structure):
+    _fields_ = [(n, _P) for n in (
+        "images", "cost_init", "arms", "cost_agg", "cost_scan", "wta", "outlier",
+        "voting", "interp", "gray", "edges", "adjusted", "subpix")]
+
+
+# name -> (restype, argtypes); every symbol include/tsm_adcensus.h declares
+SIGNATURES = {
+    "tsm_adc_create": (ctypes.c_int, [ctypes.c_int, ctypes.POINTER(_P)]),
+    "tsm_adc_destroy": (ctypes.c_int, [_P]),
+    "tsm_adc_set_disparity_range": (ctypes.c_int, [_P, ctypes.c_int, ctypes.c_int]),
+    "tsm_adc_set_strategy": (ctypes.c_int, [_P, ctypes.c_int, ctypes.c_int, ctypes.c_int]),
+    "tsm_adc_set_offset": (ctypes.c_int, [_P, ctypes.c_int]),
+    "tsm_adc_compute": (ctypes.c_int, [_P, _P, _P, ctypes.c_int, ctypes.c_int, ctypes.c_size_t,
+                                       _P, ctypes.c_size_t]),
+    "tsm_adc_compute_device": (ctypes.c_int, [_P, _P, _P, ctypes.c_int, ctypes.c_int,
+                                              ctypes.c_size_t, _P, ctypes.c_size_t, _P]),
+    "tsm_adc_compute_batch": (ctypes.c_int, [_P, ctypes.c_int, _P, _P, ctypes.c_int, ctypes.c_int,
+                                             ctypes.c_size_t, _P, ctypes.c_size_t]),
+    "tsm_adc_compute_batch_device": (ctypes.c_int, [_P, ctypes.c_int, _P, _P, ctypes.c_int,
+                                                    ctypes.c_int, ctypes.c_size_t, _P,
+                                                    ctypes.c_size_t]),
+    "tsm_adc_synchronize": (ctypes.c_int, [_P]),
+    "tsm_adc_get_params": (ctypes.c_int, [_P, ctypes.POINTER(TsmParams)]),
+    "tsm_adc_set_params": (ctypes.c_int, [_P, ctypes.POINTER(TsmParams)]),
+    "tsm_adc_get_disparity_range": (ctypes.c_int, [_P, ctypes.POINTER(ctypes.c_int),
+                                                   ctypes.POINTER(ctypes.c_int)]),
+    "tsm_adc_set_concurrency": (ctypes.c_int, [_P, ctypes.c_int]),
+    "tsm_adc_set_omp_emulation": (ctypes.c_int, [_P, ctypes.c_int]),
+    "tsm_adc_compute_debug": (ctypes.c_int, [_P, _P, _P, ctypes.c_int, ctypes.c_int,
+                                             ctypes.c_size_t, _P, ctypes.c_size_t,
+                                             ctypes.POINTER(TsmDump)]),
+    "tsm_adc_set_profiling": (ctypes.c_int, [_P, ctypes.c_int]),
+    "tsm_adc_stage_times": (ctypes.c_int, [_P, _P, _P, ctypes.c_int]),
+    "tsm_adc_reset_stage_times": (ctypes.c_int, [_P]),
+    "tsm_adc_workspace_bytes": (ctypes.c_size_t, [_P, ctypes.c_int, ctypes.c_int]),
+    "tsm_adc_last_error": (ctypes.c_char_p, [_P]),
+    "tsm_device_count": (ctypes.c_int, []),
+    "tsm_version": (ctypes.c_char_p, []),
+}
+
+_lib = None
+
+
+def load() -> ctypes.CDLL:
+    """Load the HIP library (raises if it has not been built: no CPU fallback)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise ImportError(
+            f"{LIB_PATH} not found: build the gfx950 library first "
+            "(`make lib` or `python -c 'import __graft_entry__ as g; g.build()'`)")
+    lib = ctypes.CDLL(LIB_PATH)
+    for name, (res, args) in SIGNATURES.items():
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    _lib = lib
+    return lib
+
+
+def device_count() -> int:
+    return int(load().tsm_device_count())
+
+
+def version() -> str:
+    return load().tsm_version().decode()

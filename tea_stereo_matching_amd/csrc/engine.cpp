@@ -1,0 +1,731 @@
+// engine.cpp -- host orchestration of the AD-Census pipeline on one MI355X and the
+// C ABI declared in include/tsm_adcensus.h.
+//
+// A handle (tsm_adc) holds the reference's matcher state (ADCensusImpl members,
+// ADCensus.cpp:276-295) plus a pool of per-pair workspaces, each with its own HIP
+// stream and HBM buffers sized for (H, W, L).  compute() enqueues the whole pipeline
+// without any host synchronisation inside it; batch entry points round-robin pairs over
+// the workspaces so independent pairs overlap on the device.
+#include <hip/hip_runtime.h>
+
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "../../include/tsm_adcensus.h"
+#include "tsm_launch.h"
+
+using namespace tsm;
+
+namespace {
+
+const char* kMsgRange = "[ADCensus] Set MinMaxDisparity error.";  // ADCensus.cpp:310
+const char* kMsgOffset = "[ADCensus] Offset must be positive.";    // ADCensus.cpp:326
+const char* kMsgImage = "[ADCensus] Image error.";                 // ADCensus.cpp:333
+
+// setADCensusParams, stereo_utils.cpp:271-326
+void default_params(tsm_adc_params* p, int model) {
+    std::memset(p, 0, sizeof(*p));
+    p->lambda_ad = 10.f;
+    p->census_win = 0;
+    p->lambda_census = 30.f;
+    p->lambda_hue = 1.f;
+    p->lambda_saturation = 2.5f;
+    p->lambda_intensity = 2.5f;
+    p->iterations = 4;
+    p->pi1 = 1.f;
+    p->pi2 = 3.f;
+    p->disp_tolerance = 0;
+    p->voting_thresh = 20;
+    p->voting_ratio_thresh = 0.4f;
+    p->max_search_depth = 20;
+    p->blur_kernel_size = 3;
+    p->canny_thresh1 = 30;
+    p->canny_thresh2 = 90;
+    p->canny_kernel_size = 3;
+    if (model == TSM_COLOR_RGB) {
+        p->color_thresh1 = 20;
+        p->color_thresh2 = 6;
+        p->max_length1 = 34;
+        p->max_length2 = 17;
+        p->color_diff = 15;
+    } else {
+        p->color_thresh1 = 5;
+        p->color_thresh2 = 1;
+        p->max_length1 = 17;
+        p->max_length2 = 8;
+        p->color_diff = 3;
+        p->saturation_thresh1 = 10;
+        p->saturation_thresh2 = 2;
+        p->intensity_thresh1 = 12;
+        p->intensity_thresh2 = 3;
+    }
+}
+
+struct Workspace {
+    hipStream_t stream = nullptr;
+    int H = 0, W = 0, L = 0, Lp = 0, model = -1;
+    float lambda_ad = 0, lambda_census = 0;
+    size_t bytes = 0;
+    // host-API staging
+    uint8_t* in_left = nullptr;
+    uint8_t* in_right = nullptr;
+    size_t in_cap = 0;
+    float* out_dev = nullptr;
+    // pipeline buffers
+    uint32_t* img_orig = nullptr;  // [2][H][W] packed BGR
+    uint32_t* img = nullptr;       // [2][H][W] matched images (== img_orig for RGB)
+    uint32_t* img_tmp = nullptr;   // HSI scratch
+    uint32_t* desc = nullptr;      // [2][H][W][12]
+    float* vol = nullptr;          // [2][H][W][Lp]
+    uint32_t* arms = nullptr;      // [2][H][W]
+    int32_t* ws = nullptr;         // [2][2][H][W]
+    uint8_t* gv = nullptr;         // [2][H][W]
+    uint8_t* gh = nullptr;         // [2][H][W]
+    float* lutA = nullptr;
+    float* lutB = nullptr;
+    int lutA_n = 0;
+    RefineBufs rb{};
+    std::vector<void*> allocs;
+    // profiling
+    std::vector<hipEvent_t> ev_pool;
+    std::vector<std::vector<hipEvent_t>> pending;
+};
+
+}  // namespace
+
+struct tsm_adc {
+    int device = 0;
+    int min_disparity = 0;   // ADCensus.cpp:411
+    int max_disparity = 64;  // ADCensus.cpp:412
+    int color_model = TSM_COLOR_HSI;  // ADCensus.cpp:413
+    int roi = 0, mask = 0, offset = 0;
+    tsm_adc_params params{};
+    int omp_threads = 0;
+    int concurrency = 2;
+    bool profiling = false;
+    double stage_ms[TSM_STAGE_COUNT] = {};
+    int stage_cnt[TSM_STAGE_COUNT] = {};
+    std::vector<Workspace*> ws;
+    std::string err;
+};
+
+namespace {
+
+int fail(tsm_adc* h, int code, const std::string& msg) {
+    if (h) h->err = msg;
+    return code;
+}
+
+#define HIP_OK(expr)                                                                      \
+    do {                                                                                  \
+        hipError_t e_ = (expr);                                                           \
+        if (e_ != hipSuccess)                                                             \
+            return fail(h, TSM_ERR_DEVICE, std::string(#expr) + ": " + hipGetErrorString(e_)); \
+    } while (0)
+
+int round_up4(int x) { return (x + 3) & ~3; }
+
+// Supported geometry: the aggregation LDS ring must fit 160 KiB and the per-line
+// kernels hold up to 4 float4 groups per lane.
+constexpr int kMaxLabels = 480;
+
+void free_ws(Workspace* w) {
+    for (void* p : w->allocs) hipFree(p);
+    w->allocs.clear();
+    w->bytes = 0;
+    w->H = w->W = w->L = 0;
+}
+
+int alloc(tsm_adc* h, Workspace* w, void** p, size_t bytes) {
+    bytes = (bytes + 255) & ~(size_t)255;
+    hipError_t e = hipMalloc(p, bytes);
+    if (e != hipSuccess) return fail(h, TSM_ERR_OUT_OF_MEMORY, std::string("hipMalloc: ") + hipGetErrorString(e));
+    w->allocs.push_back(*p);
+    w->bytes += bytes;
+    return TSM_OK;
+}
+
+size_t workspace_bytes(int H, int W, int L) {
+    const size_t N = (size_t)H * W, Lp = (size_t)round_up4(L);
+    size_t b = 0;
+    b += 3 * 2 * N * 4;        // img_orig, img, img_tmp
+    b += 2 * N * 12 * 4;       // desc
+    b += 2 * N * Lp * 4;       // vol
+    b += 2 * N * 4;            // arms
+    b += 4 * N * 4;            // ws
+    b += 4 * N;                // gv, gh
+    b += N * (4 * 8 + 2 * 20 + 1 * 6 + 2 * 2 + 4); // refine maps
+    return b;
+}
+
+// Host-built exp tables: the exact float arguments the reference hands to std::exp
+// (ADCensus.cpp:518 with :426-452), evaluated by the host libm once.
+void build_luts(const tsm_adc_params& p, int model, std::vector<float>& A, std::vector<float>& B) {
+    if (model == TSM_COLOR_RGB) {
+        A.resize(766);
+        for (int s = 0; s < 766; ++s) {
+            float ad = 0.f;
+            ad = (float)s;  // exact integer sum of |dB|+|dG|+|dR|
+            ad = ad / 3.f;
+            A[s] = std::exp(-ad / p.lambda_ad);
+        }
+    } else {
+        // ad = hueDiff*lambdaHue + satDiff*lambdaSat + intDiff*lambdaInt with the default
+        // lambdas (1, 2.5, 2.5) is exactly k/2 for k = 2*hue + 5*(sat+int).
+        A.resize(2805);
+        for (int k = 0; k < 2805; ++k) {
+            const float ad = (float)k / 2.f;
+            A[k] = std::exp(-ad / p.lambda_ad);
+        }
+    }
+    B.resize(188);
+    for (int c = 0; c < 187; ++c) {
+        const float cc = (float)c;
+        B[c] = std::exp(-cc / p.lambda_census);
+    }
+    B[187] = 0.f;  // exp(-inf): mask-mode census of a black centre (:459-460)
+}
+
+DevParams make_params(const tsm_adc* h, int H, int W) {
+    const tsm_adc_params& p = h->params;
+    DevParams P{};
+    P.H = H;
+    P.W = W;
+    P.minD = h->min_disparity;
+    P.maxD = h->max_disparity;
+    P.L = P.maxD - P.minD + 1;
+    P.Lp = round_up4(P.L);
+    P.color_model = h->color_model;
+    P.mask = h->mask;
+    P.censusW = p.census_win == 1 ? 7 : 9;
+    P.censusH = p.census_win == 1 ? 5 : 7;
+    P.color_thresh1 = p.color_thresh1;
+    P.color_thresh2 = p.color_thresh2;
+    P.sat_thresh1 = p.saturation_thresh1;
+    P.sat_thresh2 = p.saturation_thresh2;
+    P.int_thresh1 = p.intensity_thresh1;
+    P.int_thresh2 = p.intensity_thresh2;
+    P.max_length1 = p.max_length1;
+    P.max_length2 = p.max_length2;
+    P.color_diff = p.color_diff;
+    P.pi1 = p.pi1;
+    P.pi2 = p.pi2;
+    // computeP1P2 :954-979 (float divisions as written)
+    P.p1t[2] = p.pi1;
+    P.p2t[2] = p.pi2;
+    P.p1t[1] = p.pi1 / 4.f;
+    P.p2t[1] = p.pi2 / 4.f;
+    P.p1t[0] = p.pi1 / 10.f;
+    P.p2t[0] = p.pi2 / 10.f;
+    P.disp_tolerance = p.disp_tolerance;
+    P.voting_thresh = p.voting_thresh;
+    P.voting_ratio = p.voting_ratio_thresh;
+    P.max_search_depth = p.max_search_depth;
+    // Canny(…, low, high): cvFloor of the (swapped if needed) thresholds
+    double lo = p.canny_thresh1, hi = p.canny_thresh2;
+    if (lo > hi) std::swap(lo, hi);
+    P.canny_low = (int)std::floor(lo);
+    P.canny_high = (int)std::floor(hi);
+    P.omp_threads = h->omp_threads;
+    return P;
+}
+
+int ensure_workspace(tsm_adc* h, Workspace* w, int H, int W) {
+    const int L = h->max_disparity - h->min_disparity + 1;
+    if (w->stream == nullptr) HIP_OK(hipStreamCreateWithFlags(&w->stream, hipStreamNonBlocking));
+    const tsm_adc_params& p = h->params;
+    if (w->H == H && w->W == W && w->L == L && w->model == h->color_model &&
+        w->lambda_ad == p.lambda_ad && w->lambda_census == p.lambda_census)
+        return TSM_OK;
+    HIP_OK(hipStreamSynchronize(w->stream));
+    free_ws(w);
+    const size_t N = (size_t)H * W;
+    const int Lp = round_up4(L);
+    int rc;
+#define A(ptr, bytes)                                                      \
+    if ((rc = alloc(h, w, (void**)&(ptr), (bytes))) != TSM_OK) { free_ws(w); return rc; }
+    A(w->img_orig, 2 * N * 4);
+    if (h->color_model == TSM_COLOR_HSI) {
+        A(w->img, 2 * N * 4);
+        A(w->img_tmp, 2 * N * 4);
+    } else {
+        w->img = w->img_orig;
+    }
+    A(w->desc, 2 * N * 12 * 4);
+    A(w->vol, 2 * N * (size_t)Lp * 4);
+    A(w->arms, 2 * N * 4);
+    A(w->ws, 4 * N * 4);
+    A(w->gv, 2 * N);
+    A(w->gh, 2 * N);
+    RefineBufs& B = w->rb;
+    A(B.disp0, N * 4);
+    A(B.disp1, N * 4);
+    A(B.dm, N * 4);
+    A(B.dtmp, N * 4);
+    A(B.vote, N * 4);
+    A(B.samples, N * 20 * 2);
+    A(B.flags, N);
+    A(B.out_pos, N * 4);
+    A(B.out_list, N * 4);
+    A(B.hi_list, N * 4);
+    A(B.bsum, 2 * refine_scan_blocks((int)N) * 4 + 64);
+    A(B.counts, 16);
+    A(B.gray, N);
+    A(B.gray_eq, N);
+    A(B.hist, (256 + 64) * 4);
+    A(B.blurred, N);
+    A(B.dx, N * 2);
+    A(B.dy, N * 2);
+    A(B.mag, N * 4);
+    A(B.map, N);
+    A(B.label, N * 4);
+    A(B.strong, N);
+    A(B.edges, N);
+    A(B.subpix, N * 4);
+    std::vector<float> la, lb;
+    build_luts(p, h->color_model, la, lb);
+    A(w->lutA, la.size() * 4);
+    A(w->lutB, lb.size() * 4);
+#undef A
+    w->lutA_n = (int)la.size();
+    HIP_OK(hipMemcpy(w->lutA, la.data(), la.size() * 4, hipMemcpyHostToDevice));
+    HIP_OK(hipMemcpy(w->lutB, lb.data(), lb.size() * 4, hipMemcpyHostToDevice));
+    // padded lanes of the volume are never read as labels; keep them defined anyway
+    HIP_OK(hipMemset(w->vol, 0, 2 * N * (size_t)Lp * 4));
+    w->H = H;
+    w->W = W;
+    w->L = L;
+    w->Lp = Lp;
+    w->model = h->color_model;
+    w->lambda_ad = p.lambda_ad;
+    w->lambda_census = p.lambda_census;
+    return TSM_OK;
+}
+
+int ensure_input_staging(tsm_adc* h, Workspace* w, int H, size_t step, int W) {
+    const size_t need = (size_t)H * step;
+    if (w->in_cap < need) {
+        if (w->in_left) { hipFree(w->in_left); w->in_left = nullptr; }
+        if (w->in_right) { hipFree(w->in_right); w->in_right = nullptr; }
+        if (w->out_dev) { hipFree(w->out_dev); w->out_dev = nullptr; }
+        HIP_OK(hipMalloc((void**)&w->in_left, need));
+        HIP_OK(hipMalloc((void**)&w->in_right, need));
+        w->in_cap = need;
+    }
+    if (w->out_dev == nullptr) HIP_OK(hipMalloc((void**)&w->out_dev, (size_t)H * W * 4 + 256));
+    return TSM_OK;
+}
+
+// Validation shared by every compute entry (ADCensus.cpp:332-340).
+int validate(tsm_adc* h, const void* l, const void* r, int rows, int cols, size_t step) {
+    if (!h) return TSM_ERR_ARGUMENT;
+    if (!l || !r || rows <= 0 || cols <= 0 || step < (size_t)cols * 3)
+        return fail(h, TSM_ERR_IMAGE, kMsgImage);
+    if (h->roi || h->mask) h->max_disparity = cols / 2;  // :339-340 (persists, as in the reference)
+    const int L = h->max_disparity - h->min_disparity + 1;
+    if (L <= 1 || L > kMaxLabels)
+        return fail(h, TSM_ERR_UNSUPPORTED, "disparity range of " + std::to_string(L) + " labels is outside [2, " + std::to_string(kMaxLabels) + "]");
+    if (h->min_disparity < 0)
+        return fail(h, TSM_ERR_UNSUPPORTED, "negative minimum disparity (reference indexes its volume out of bounds, ADCensus.cpp:1398-1404)");
+    if (h->params.census_win == 0 && (h->params.lambda_hue != 1.f || h->params.lambda_saturation != 2.5f ||
+                                      h->params.lambda_intensity != 2.5f) && h->color_model == TSM_COLOR_HSI)
+        return fail(h, TSM_ERR_UNSUPPORTED, "HSI AD lambdas other than (1, 2.5, 2.5)");
+    return TSM_OK;
+}
+
+struct Prof {
+    Workspace* w;
+    std::vector<hipEvent_t> ev;
+};
+
+hipEvent_t take_event(Workspace* w) {
+    if (!w->ev_pool.empty()) {
+        hipEvent_t e = w->ev_pool.back();
+        w->ev_pool.pop_back();
+        return e;
+    }
+    hipEvent_t e;
+    hipEventCreate(&e);
+    return e;
+}
+
+// Enqueue the full pipeline for one pair on workspace w.  d_left/d_right: device BGR
+// with `step`; d_out: device fp32 with out_step.  No host synchronisation.
+int run_pipeline(tsm_adc* h, Workspace* w, const uint8_t* d_left, const uint8_t* d_right,
+                 size_t step, float* d_out, size_t out_step, const tsm_adc_dump* dump,
+                 hipStream_t st) {
+    const int H = w->H, W = w->W;
+    const DevParams P = make_params(h, H, W);
+    const size_t N = (size_t)H * W;
+    std::vector<hipEvent_t> ev;
+    auto mark = [&]() {
+        if (!h->profiling) return;
+        hipEvent_t e = take_event(w);
+        hipEventRecord(e, st);
+        ev.push_back(e);
+    };
+    auto dump_vol = [&](float* dst, int views) -> int {
+        float* tmp = nullptr;
+        HIP_OK(hipMalloc((void**)&tmp, (size_t)views * P.L * N * 4));
+        launch_vol_to_ref(w->vol, tmp, views, P, st);
+        HIP_OK(hipMemcpyAsync(dst, tmp, (size_t)views * P.L * N * 4, hipMemcpyDeviceToHost, st));
+        HIP_OK(hipStreamSynchronize(st));
+        hipFree(tmp);
+        return TSM_OK;
+    };
+    auto d2h = [&](void* dst, const void* src, size_t bytes) -> int {
+        HIP_OK(hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToHost, st));
+        HIP_OK(hipStreamSynchronize(st));
+        return TSM_OK;
+    };
+    int rc;
+
+    mark();
+    // --- prep: pack (+HSI), census descriptors -------------------------------------
+    launch_pack(d_left, d_right, step, H, W, w->img_orig, st);
+    if (h->color_model == TSM_COLOR_HSI)
+        launch_hsi(w->img_orig, w->img_tmp, w->img, H, W, (h->roi || h->mask) ? 1 : 0, st);
+    launch_census(w->img, w->desc, P, st);
+    mark();
+    // --- cost volume -------------------------------------------------------------
+    if (launch_cost_volume(w->img, w->desc, w->lutA, w->lutA_n, w->lutB, w->vol, P, st) != 0)
+        return fail(h, TSM_ERR_UNSUPPORTED, "cost volume: label count");
+    mark();
+    if (dump && dump->images) {
+        std::vector<uint32_t> tmp(2 * N);
+        if ((rc = d2h(tmp.data(), w->img, 2 * N * 4)) != TSM_OK) return rc;
+        for (size_t i = 0; i < 2 * N; ++i) {
+            dump->images[3 * i + 0] = tmp[i] & 0xff;
+            dump->images[3 * i + 1] = (tmp[i] >> 8) & 0xff;
+            dump->images[3 * i + 2] = (tmp[i] >> 16) & 0xff;
+        }
+    }
+    if (dump && dump->cost_init && (rc = dump_vol(dump->cost_init, 2)) != TSM_OK) return rc;
+    // --- arms, window sizes, colour gradients ----------------------------------------
+    launch_arms(w->img, w->arms, P, st);
+    launch_window_sizes(w->arms, w->ws, P, st);
+    launch_color_grad(w->img, w->gv, w->gh, P, st);
+    mark();
+    if (dump && dump->arms) {
+        int32_t* tmp = nullptr;
+        HIP_OK(hipMalloc((void**)&tmp, 8 * N * 4));
+        launch_arms_to_ref(w->arms, tmp, P, st);
+        rc = d2h(dump->arms, tmp, 8 * N * 4);
+        hipFree(tmp);
+        if (rc != TSM_OK) return rc;
+    }
+    // --- aggregation: iterations x (1-D pass, 1-D pass + divide) -----------------------
+    {
+        bool hf = true;  // costAggregate :776-782
+        for (int it = 0; it < h->params.iterations; ++it) {
+            const int32_t* wsel = w->ws + (hf ? 0 : N);  // ws[v][hf?0:1] via the per-view stride 2N
+            if (launch_agg_line(w->vol, w->arms, nullptr, hf ? 1 : 0, P, st) != 0 ||
+                launch_agg_line(w->vol, w->arms, wsel, hf ? 0 : 1, P, st) != 0)
+                return fail(h, TSM_ERR_UNSUPPORTED, "aggregation: label count");
+            hf = !hf;
+        }
+    }
+    mark();
+    if (dump && dump->cost_agg && (rc = dump_vol(dump->cost_agg, 2)) != TSM_OK) return rc;
+    // --- scanline (+ fused WTA in the last pass) -------------------------------------
+    const bool keep_view1 = dump && dump->cost_scan;
+    if (launch_scan_vertical(w->vol, w->gv, w->img, +1, P, st) != 0 ||
+        launch_scan_vertical(w->vol, w->gv, w->img, -1, P, st) != 0 ||
+        launch_scan_horizontal(w->vol, w->gh, w->img, +1, nullptr, 1, P, st) != 0 ||
+        launch_scan_horizontal(w->vol, w->gh, w->img, -1, w->rb.disp0, keep_view1 ? 1 : 0, P, st) != 0)
+        return fail(h, TSM_ERR_UNSUPPORTED, "scanline: label count");
+    mark();
+    if (keep_view1 && (rc = dump_vol(dump->cost_scan, 2)) != TSM_OK) return rc;
+    if (dump && dump->wta && (rc = d2h(dump->wta, w->rb.disp0, 2 * N * 4)) != TSM_OK) return rc;
+    // --- refinement --------------------------------------------------------------------
+    launch_outlier(w->rb, P, st);
+    if (dump && dump->outlier && (rc = d2h(dump->outlier, w->rb.dm, N * 4)) != TSM_OK) return rc;
+    {
+        int hf = 0;  // multiOptimize :1382-1387
+        for (int i = 0; i < 5; ++i) {
+            launch_region_voting(w->rb, w->arms, hf, P, st);
+            hf = !hf;
+        }
+    }
+    if (dump && dump->voting && (rc = d2h(dump->voting, w->rb.dm, N * 4)) != TSM_OK) return rc;
+    launch_interpolation(w->rb, w->img, P, st);
+    if (dump && dump->interp && (rc = d2h(dump->interp, w->rb.dm, N * 4)) != TSM_OK) return rc;
+    launch_discontinuity(w->rb, w->vol, P, st);
+    if (dump && dump->gray && (rc = d2h(dump->gray, w->rb.gray_eq, N)) != TSM_OK) return rc;
+    if (dump && dump->edges && (rc = d2h(dump->edges, w->rb.edges, N)) != TSM_OK) return rc;
+    if (dump && dump->adjusted && (rc = d2h(dump->adjusted, w->rb.dm, N * 4)) != TSM_OK) return rc;
+    launch_subpixel_median(w->rb, w->vol, w->img_orig, d_out, out_step, (h->roi || h->mask) ? 1 : 0,
+                           h->offset, P, st);
+    if (dump && dump->subpix && (rc = d2h(dump->subpix, w->rb.subpix, N * 4)) != TSM_OK) return rc;
+    mark();
+    HIP_OK(hipGetLastError());
+    if (h->profiling) w->pending.push_back(ev);
+    return TSM_OK;
+}
+
+// Fold finished per-pair events into the handle's stage totals (call after sync).
+void collect_profile(tsm_adc* h, Workspace* w) {
+    for (auto& ev : w->pending) {
+        for (size_t k = 0; k + 1 < ev.size() && k < TSM_STAGE_COUNT; ++k) {
+            float ms = 0.f;
+            if (hipEventElapsedTime(&ms, ev[k], ev[k + 1]) == hipSuccess) {
+                h->stage_ms[k] += ms;
+                h->stage_cnt[k] += 1;
+            }
+        }
+        for (hipEvent_t e : ev) w->ev_pool.push_back(e);
+    }
+    w->pending.clear();
+}
+
+int ensure_pool(tsm_adc* h, int n) {
+    while ((int)h->ws.size() < n) h->ws.push_back(new Workspace());
+    return TSM_OK;
+}
+
+int set_device(tsm_adc* h) {
+    HIP_OK(hipSetDevice(h->device));
+    return TSM_OK;
+}
+
+}  // namespace
+
+// ============================================================================
+// C ABI
+// ============================================================================
+extern "C" {
+
+int tsm_adc_create(int device, tsm_adc** out) {
+    if (!out) return TSM_ERR_ARGUMENT;
+    *out = nullptr;
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess || n <= 0) return TSM_ERR_DEVICE;
+    if (device < 0 || device >= n) return TSM_ERR_ARGUMENT;
+    tsm_adc* h = new tsm_adc();
+    h->device = device;
+    default_params(&h->params, h->color_model);
+    *out = h;
+    return TSM_OK;
+}
+
+int tsm_adc_destroy(tsm_adc* h) {
+    if (!h) return TSM_ERR_ARGUMENT;
+    hipSetDevice(h->device);
+    for (Workspace* w : h->ws) {
+        if (w->stream) hipStreamSynchronize(w->stream);
+        free_ws(w);
+        if (w->in_left) hipFree(w->in_left);
+        if (w->in_right) hipFree(w->in_right);
+        if (w->out_dev) hipFree(w->out_dev);
+        for (auto& ev : w->pending) for (hipEvent_t e : ev) hipEventDestroy(e);
+        for (hipEvent_t e : w->ev_pool) hipEventDestroy(e);
+        if (w->stream) hipStreamDestroy(w->stream);
+        delete w;
+    }
+    delete h;
+    return TSM_OK;
+}
+
+int tsm_adc_set_disparity_range(tsm_adc* h, int mn, int mx) {
+    if (!h) return TSM_ERR_ARGUMENT;
+    if ((long long)mn * (long long)mx < 0 || mn >= mx) return fail(h, TSM_ERR_DISPARITY_RANGE, kMsgRange);
+    h->min_disparity = mn;
+    h->max_disparity = mx;
+    return TSM_OK;
+}
+
+int tsm_adc_get_disparity_range(const tsm_adc* h, int* mn, int* mx) {
+    if (!h || !mn || !mx) return TSM_ERR_ARGUMENT;
+    *mn = h->min_disparity;
+    *mx = h->max_disparity;
+    return TSM_OK;
+}
+
+int tsm_adc_set_strategy(tsm_adc* h, int model, int roi, int mask) {
+    if (!h) return TSM_ERR_ARGUMENT;
+    if (model != TSM_COLOR_RGB && model != TSM_COLOR_HSI) return fail(h, TSM_ERR_ARGUMENT, "unknown color model");
+    h->color_model = model;
+    default_params(&h->params, model);  // m_paMatching = ADCensusParams(colorModel)
+    h->roi = roi ? 1 : 0;
+    h->mask = mask ? 1 : 0;
+    return TSM_OK;
+}
+
+int tsm_adc_set_offset(tsm_adc* h, int offset) {
+    if (!h) return TSM_ERR_ARGUMENT;
+    if (offset < 0) return fail(h, TSM_ERR_OFFSET, kMsgOffset);
+    h->offset = offset;
+    return TSM_OK;
+}
+
+int tsm_adc_get_params(const tsm_adc* h, tsm_adc_params* out) {
+    if (!h || !out) return TSM_ERR_ARGUMENT;
+    *out = h->params;
+    return TSM_OK;
+}
+
+int tsm_adc_set_params(tsm_adc* h, const tsm_adc_params* in) {
+    if (!h || !in) return TSM_ERR_ARGUMENT;
+    if (in->census_win != 0 && in->census_win != 1) return fail(h, TSM_ERR_ARGUMENT, "census_win must be 0 (9x7) or 1 (7x5)");
+    if (in->max_length1 < 1 || in->max_length1 > 128) return fail(h, TSM_ERR_UNSUPPORTED, "max_length1 outside [1, 128]");
+    if (in->voting_thresh > 20 || in->voting_thresh < 0) return fail(h, TSM_ERR_UNSUPPORTED, "voting_thresh outside [0, 20]");
+    h->params = *in;
+    return TSM_OK;
+}
+
+int tsm_adc_set_concurrency(tsm_adc* h, int n) {
+    if (!h || n < 1 || n > 16) return TSM_ERR_ARGUMENT;
+    h->concurrency = n;
+    return TSM_OK;
+}
+
+int tsm_adc_set_omp_emulation(tsm_adc* h, int threads) {
+    if (!h || threads < 0) return TSM_ERR_ARGUMENT;
+    h->omp_threads = threads;
+    return TSM_OK;
+}
+
+int tsm_adc_set_profiling(tsm_adc* h, int enable) {
+    if (!h) return TSM_ERR_ARGUMENT;
+    h->profiling = enable != 0;
+    return TSM_OK;
+}
+
+int tsm_adc_stage_times(tsm_adc* h, double* ms, int* counts, int n) {
+    if (!h) return TSM_ERR_ARGUMENT;
+    for (int k = 0; k < n && k < TSM_STAGE_COUNT; ++k) {
+        if (ms) ms[k] = h->stage_ms[k];
+        if (counts) counts[k] = h->stage_cnt[k];
+    }
+    return TSM_OK;
+}
+
+int tsm_adc_reset_stage_times(tsm_adc* h) {
+    if (!h) return TSM_ERR_ARGUMENT;
+    for (int k = 0; k < TSM_STAGE_COUNT; ++k) { h->stage_ms[k] = 0; h->stage_cnt[k] = 0; }
+    return TSM_OK;
+}
+
+size_t tsm_adc_workspace_bytes(const tsm_adc* h, int rows, int cols) {
+    if (!h || rows <= 0 || cols <= 0) return 0;
+    const int maxd = (h->roi || h->mask) ? cols / 2 : h->max_disparity;
+    return workspace_bytes(rows, cols, maxd - h->min_disparity + 1);
+}
+
+const char* tsm_adc_last_error(const tsm_adc* h) { return h ? h->err.c_str() : "null handle"; }
+
+int tsm_device_count(void) {
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess) return 0;
+    return n;
+}
+
+const char* tsm_version(void) { return "tea_stereo_matching_amd 0.1.0 (gfx950)"; }
+
+int tsm_adc_synchronize(tsm_adc* h) {
+    if (!h) return TSM_ERR_ARGUMENT;
+    int rc;
+    if ((rc = set_device(h)) != TSM_OK) return rc;
+    for (Workspace* w : h->ws) {
+        if (!w->stream) continue;
+        HIP_OK(hipStreamSynchronize(w->stream));
+        collect_profile(h, w);
+    }
+    return TSM_OK;
+}
+
+int tsm_adc_compute_device(tsm_adc* h, const uint8_t* dl, const uint8_t* dr, int rows, int cols,
+                           size_t step, float* dout, size_t out_step, void* stream) {
+    int rc = validate(h, dl, dr, rows, cols, step);
+    if (rc != TSM_OK) return rc;
+    if (!dout || out_step < (size_t)cols * 4) return fail(h, TSM_ERR_ARGUMENT, "output buffer");
+    if ((rc = set_device(h)) != TSM_OK) return rc;
+    ensure_pool(h, 1);
+    Workspace* w = h->ws[0];
+    if ((rc = ensure_workspace(h, w, rows, cols)) != TSM_OK) return rc;
+    hipStream_t st = stream ? (hipStream_t)stream : w->stream;
+    return run_pipeline(h, w, dl, dr, step, dout, out_step, nullptr, st);
+}
+
+static int compute_host(tsm_adc* h, const uint8_t* l, const uint8_t* r, int rows, int cols,
+                        size_t step, float* out, size_t out_step, const tsm_adc_dump* dump) {
+    int rc = validate(h, l, r, rows, cols, step);
+    if (rc != TSM_OK) return rc;
+    if (!out || out_step < (size_t)cols * 4) return fail(h, TSM_ERR_ARGUMENT, "output buffer");
+    if ((rc = set_device(h)) != TSM_OK) return rc;
+    ensure_pool(h, 1);
+    Workspace* w = h->ws[0];
+    if ((rc = ensure_workspace(h, w, rows, cols)) != TSM_OK) return rc;
+    if ((rc = ensure_input_staging(h, w, rows, (size_t)cols * 3, cols)) != TSM_OK) return rc;
+    const size_t dstep = (size_t)cols * 3;
+    HIP_OK(hipMemcpy2DAsync(w->in_left, dstep, l, step, dstep, rows, hipMemcpyHostToDevice, w->stream));
+    HIP_OK(hipMemcpy2DAsync(w->in_right, dstep, r, step, dstep, rows, hipMemcpyHostToDevice, w->stream));
+    if ((rc = run_pipeline(h, w, w->in_left, w->in_right, dstep, w->out_dev, (size_t)cols * 4, dump, w->stream)) != TSM_OK)
+        return rc;
+    HIP_OK(hipMemcpy2DAsync(out, out_step, w->out_dev, (size_t)cols * 4, (size_t)cols * 4, rows,
+                            hipMemcpyDeviceToHost, w->stream));
+    HIP_OK(hipStreamSynchronize(w->stream));
+    collect_profile(h, w);
+    return TSM_OK;
+}
+
+int tsm_adc_compute(tsm_adc* h, const uint8_t* l, const uint8_t* r, int rows, int cols, size_t step,
+                    float* out, size_t out_step) {
+    return compute_host(h, l, r, rows, cols, step, out, out_step, nullptr);
+}
+
+int tsm_adc_compute_debug(tsm_adc* h, const uint8_t* l, const uint8_t* r, int rows, int cols,
+                          size_t step, float* out, size_t out_step, tsm_adc_dump* dump) {
+    return compute_host(h, l, r, rows, cols, step, out, out_step, dump);
+}
+
+int tsm_adc_compute_batch_device(tsm_adc* h, int n, const uint8_t* const* dls,
+                                 const uint8_t* const* drs, int rows, int cols, size_t step,
+                                 float* const* douts, size_t out_step) {
+    if (!h || n < 0 || (n > 0 && (!dls || !drs || !douts))) return TSM_ERR_ARGUMENT;
+    int rc;
+    if ((rc = set_device(h)) != TSM_OK) return rc;
+    const int S = h->concurrency;
+    ensure_pool(h, S);
+    for (int i = 0; i < n; ++i) {
+        if ((rc = validate(h, dls[i], drs[i], rows, cols, step)) != TSM_OK) return rc;
+        Workspace* w = h->ws[i % S];
+        if ((rc = ensure_workspace(h, w, rows, cols)) != TSM_OK) return rc;
+        if ((rc = run_pipeline(h, w, dls[i], drs[i], step, douts[i], out_step, nullptr, w->stream)) != TSM_OK)
+            return rc;
+    }
+    return tsm_adc_synchronize(h);
+}
+
+int tsm_adc_compute_batch(tsm_adc* h, int n, const uint8_t* const* ls, const uint8_t* const* rs,
+                          int rows, int cols, size_t step, float* const* outs, size_t out_step) {
+    if (!h || n < 0 || (n > 0 && (!ls || !rs || !outs))) return TSM_ERR_ARGUMENT;
+    int rc;
+    if ((rc = set_device(h)) != TSM_OK) return rc;
+    const int S = h->concurrency;
+    ensure_pool(h, S);
+    const size_t dstep = (size_t)cols * 3;
+    for (int i0 = 0; i0 < n; i0 += S) {
+        const int i1 = std::min(n, i0 + S);
+        for (int i = i0; i < i1; ++i) {
+            if ((rc = validate(h, ls[i], rs[i], rows, cols, step)) != TSM_OK) return rc;
+            if (!outs[i] || out_step < (size_t)cols * 4) return fail(h, TSM_ERR_ARGUMENT, "output buffer");
+            Workspace* w = h->ws[i - i0];
+            if ((rc = ensure_workspace(h, w, rows, cols)) != TSM_OK) return rc;
+            if ((rc = ensure_input_staging(h, w, rows, dstep, cols)) != TSM_OK) return rc;
+            HIP_OK(hipMemcpy2DAsync(w->in_left, dstep, ls[i], step, dstep, rows, hipMemcpyHostToDevice, w->stream));
+            HIP_OK(hipMemcpy2DAsync(w->in_right, dstep, rs[i], step, dstep, rows, hipMemcpyHostToDevice, w->stream));
+            if ((rc = run_pipeline(h, w, w->in_left, w->in_right, dstep, w->out_dev, (size_t)cols * 4, nullptr, w->stream)) != TSM_OK)
+                return rc;
+            HIP_OK(hipMemcpy2DAsync(outs[i], out_step, w->out_dev, (size_t)cols * 4, (size_t)cols * 4,
+                                    rows, hipMemcpyDeviceToHost, w->stream));
+        }
+        if ((rc = tsm_adc_synchronize(h)) != TSM_OK) return rc;
+    }
+    return TSM_OK;
+}
+
+}  // extern "C"

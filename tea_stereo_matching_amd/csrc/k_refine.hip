@@ -1,0 +1,650 @@
+// k_refine.hip -- step 4 of AD-Census on gfx950: multi-step refinement
+// (multiOptimize, ADCensus.cpp:1376-1392).  All maps are H x W int32/u8/fp32; these
+// kernels move ~1-2 % of the bytes of the cost-volume stages.
+//
+//   outlierElimination  :1013-1044   per pixel
+//   regionVoting x5     :1046-1159   per outlier; the reference's raster-order vote
+//                                    histogram CARRY (cleared only by an outlier with
+//                                    vote > votingThresh) is restated as a segmented
+//                                    scan: a high-vote outlier's histogram = its own
+//                                    samples + the samples of every low-vote outlier
+//                                    since the previous high-vote outlier.
+//   properInterpolation :1161-1239   per outlier
+//   discontinuityAdj.   :1256-1342   equalizeHist + blur 3x3 + Canny(30,90,3,L1)
+//                                    (OpenCV 4.x semantics) -> edge-pixel adjustment;
+//                                    Canny hysteresis as lock-free union-find
+//   subpixelEnhancement :1344-1374   parabola fit + medianBlur 3x3 (fp32, replicate)
+#include "tsm_device.h"
+#include "tsm_launch.h"
+
+namespace tsm {
+
+constexpr int kMaxSamples = 20; // = votingThresh: a low-vote outlier holds <= 20 samples
+
+// ---------------------------------------------------------------------------
+// outlier elimination (LR check)
+// ---------------------------------------------------------------------------
+__global__ void k_outlier(const int32_t* __restrict__ dl, const int32_t* __restrict__ dr,
+                          int32_t* __restrict__ out, DevParams P) {
+    const int x = blockIdx.x * blockDim.x + threadIdx.x;
+    const int y = blockIdx.y;
+    const int W = P.W;
+    if (x >= W) return;
+    const int32_t* r = dr + (size_t)y * W;
+    int d = dl[(size_t)y * W + x];
+    if (x - d < 0 || iabs_(d - r[x - d]) > P.disp_tolerance) {
+        bool occ = true;
+        for (int k = P.minD; k <= P.maxD; ++k) {
+            if (x - k >= 0 && k == r[x - k]) { occ = false; break; }
+        }
+        d = occ ? -1 : -2; // m_occlusionValue / m_mismatchValue (:415-416)
+    }
+    out[(size_t)y * W + x] = d;
+}
+
+// ---------------------------------------------------------------------------
+// region voting
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ void region_arms(uint32_t a, bool hf, int& oA, int& oB, int& iA, int& iB) {
+    const int up = a & 0xff, dn = (a >> 8) & 0xff, lf = (a >> 16) & 0xff, rt = (a >> 24) & 0xff;
+    if (hf) { oA = up; oB = dn; iA = lf; iB = rt; }
+    else { oA = lf; oB = rt; iA = up; iB = dn; }
+}
+
+// Per pixel: vote count of outliers (+ up to 20 samples for low-vote ones) and flags
+// (bit0 outlier, bit1 high-vote).
+__global__ void k_vote_count(const int32_t* __restrict__ disp, const uint32_t* __restrict__ arms,
+                             int32_t* __restrict__ vote, uint16_t* __restrict__ samples,
+                             uint8_t* __restrict__ flags, int hf, DevParams P) {
+    const int x = blockIdx.x * blockDim.x + threadIdx.x;
+    const int y = blockIdx.y;
+    const int W = P.W;
+    if (x >= W) return;
+    const size_t idx = (size_t)y * W + x;
+    const int minD = P.minD;
+    if (disp[idx] >= minD) { flags[idx] = 0; vote[idx] = 0; return; }
+    int oA, oB, iA, iB;
+    region_arms(arms[idx], hf, oA, oB, iA, iB);
+    int cnt = 0;
+    uint16_t* smp = samples + idx * kMaxSamples;
+    for (int o = -oA; o <= oB; ++o) {
+        const int yy0 = hf ? y + o : y, xx0 = hf ? x : x + o;
+        int a1, b1, a2, b2;
+        region_arms(arms[(size_t)yy0 * W + xx0], hf, a1, b1, a2, b2);
+        for (int i = -a2; i <= b2; ++i) {
+            const int yy = hf ? y + o : y + i;
+            const int xx = hf ? x + i : x + o;
+            const int dv = disp[(size_t)yy * W + xx];
+            if (dv >= minD) {
+                if (cnt < kMaxSamples) smp[cnt] = (uint16_t)(dv - minD);
+                cnt++;
+            }
+        }
+    }
+    vote[idx] = cnt;
+    flags[idx] = 1 | (cnt > P.voting_thresh ? 2 : 0);
+}
+
+// Device-wide exclusive scan of the two flag counters in raster order:
+//   out_pos[p]  = # outliers before p        out_list[out_pos[p]] = p
+//   hi_list[r]  = r-th high-vote outlier      counts = {#outliers, #high-vote}
+constexpr int SC_THREADS = 256, SC_ITEMS = 16, SC_BLOCK = SC_THREADS * SC_ITEMS;
+
+__device__ __forceinline__ void block_scan2(int& a, int& b, int* sa, int* sb) {
+    // inclusive scan over the block of (a, b), returns exclusive prefix; totals in sa/sb[SC_THREADS]
+    const int t = threadIdx.x;
+    sa[t] = a;
+    sb[t] = b;
+    __syncthreads();
+    for (int off = 1; off < SC_THREADS; off <<= 1) {
+        int xa = 0, xb = 0;
+        if (t >= off) { xa = sa[t - off]; xb = sb[t - off]; }
+        __syncthreads();
+        sa[t] += xa;
+        sb[t] += xb;
+        __syncthreads();
+    }
+    const int ia = sa[t], ib = sb[t];
+    a = ia - a;
+    b = ib - b;
+}
+
+__global__ void k_scan_count(const uint8_t* __restrict__ flags, int n, int32_t* __restrict__ bsum) {
+    __shared__ int sa[SC_THREADS], sb[SC_THREADS];
+    const int base = blockIdx.x * SC_BLOCK + threadIdx.x * SC_ITEMS;
+    int a = 0, b = 0;
+    for (int k = 0; k < SC_ITEMS; ++k) {
+        const int p = base + k;
+        if (p < n) { const uint8_t f = flags[p]; a += f & 1; b += (f >> 1) & 1; }
+    }
+    block_scan2(a, b, sa, sb);
+    if (threadIdx.x == SC_THREADS - 1) {
+        bsum[2 * blockIdx.x] = sa[SC_THREADS - 1];
+        bsum[2 * blockIdx.x + 1] = sb[SC_THREADS - 1];
+    }
+}
+
+__global__ void k_scan_blocks(int32_t* __restrict__ bsum, int nb, int32_t* __restrict__ counts) {
+    // single block: exclusive scan of nb block totals (nb <= 1024 * 8)
+    __shared__ int sa[SC_THREADS], sb[SC_THREADS];
+    const int per = (nb + SC_THREADS - 1) / SC_THREADS;
+    const int b0 = threadIdx.x * per;
+    int a = 0, b = 0;
+    for (int k = 0; k < per; ++k)
+        if (b0 + k < nb) { a += bsum[2 * (b0 + k)]; b += bsum[2 * (b0 + k) + 1]; }
+    block_scan2(a, b, sa, sb);
+    for (int k = 0; k < per; ++k) {
+        if (b0 + k < nb) {
+            const int ta = bsum[2 * (b0 + k)], tb = bsum[2 * (b0 + k) + 1];
+            bsum[2 * (b0 + k)] = a;
+            bsum[2 * (b0 + k) + 1] = b;
+            a += ta;
+            b += tb;
+        }
+    }
+    if (threadIdx.x == SC_THREADS - 1) { counts[0] = sa[SC_THREADS - 1]; counts[1] = sb[SC_THREADS - 1]; }
+}
+
+__global__ void k_scan_scatter(const uint8_t* __restrict__ flags, int n,
+                               const int32_t* __restrict__ bsum, int32_t* __restrict__ out_pos,
+                               int32_t* __restrict__ out_list, int32_t* __restrict__ hi_list) {
+    __shared__ int sa[SC_THREADS], sb[SC_THREADS];
+    const int base = blockIdx.x * SC_BLOCK + threadIdx.x * SC_ITEMS;
+    int a = 0, b = 0;
+    for (int k = 0; k < SC_ITEMS; ++k) {
+        const int p = base + k;
+        if (p < n) { const uint8_t f = flags[p]; a += f & 1; b += (f >> 1) & 1; }
+    }
+    block_scan2(a, b, sa, sb);
+    a += bsum[2 * blockIdx.x];
+    b += bsum[2 * blockIdx.x + 1];
+    for (int k = 0; k < SC_ITEMS; ++k) {
+        const int p = base + k;
+        if (p >= n) break;
+        const uint8_t f = flags[p];
+        if (f & 1) { out_pos[p] = a; out_list[a] = p; a++; }
+        if (f & 2) { hi_list[b] = p; b++; }
+    }
+}
+
+// One wave per high-vote outlier: LDS histogram of its own region + carried samples,
+// then the first argmax and the ratio test (:1137-1153).
+constexpr int VD_THREADS = 256;
+
+__global__ __launch_bounds__(VD_THREADS) void k_vote_decide(
+    const int32_t* __restrict__ disp, int32_t* __restrict__ dtmp, const uint32_t* __restrict__ arms,
+    const int32_t* __restrict__ vote, const uint16_t* __restrict__ samples,
+    const int32_t* __restrict__ out_pos, const int32_t* __restrict__ out_list,
+    const int32_t* __restrict__ hi_list, const int32_t* __restrict__ counts, int hf, DevParams P) {
+    extern __shared__ int hist_all[];
+    const int L = P.L, W = P.W, minD = P.minD;
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    int* hist = hist_all + wave * L;
+    const int nhi = counts[1];
+    const int nwaves = gridDim.x * (VD_THREADS / 64);
+    for (int r = blockIdx.x * (VD_THREADS / 64) + wave; r < nhi; r += nwaves) {
+        for (int d = lane; d < L; d += 64) hist[d] = 0;
+        __builtin_amdgcn_wave_barrier();
+        const int p = hi_list[r];
+        const int y = p / W, x = p - y * W;
+        int oA, oB, iA, iB;
+        region_arms(arms[p], hf, oA, oB, iA, iB);
+        for (int o = -oA + lane; o <= oB; o += 64) {
+            const int yy0 = hf ? y + o : y, xx0 = hf ? x : x + o;
+            int a1, b1, a2, b2;
+            region_arms(arms[(size_t)yy0 * W + xx0], hf, a1, b1, a2, b2);
+            for (int i = -a2; i <= b2; ++i) {
+                const int yy = hf ? y + o : y + i;
+                const int xx = hf ? x + i : x + o;
+                const int dv = disp[(size_t)yy * W + xx];
+                if (dv >= minD) atomicAdd(&hist[dv - minD], 1);
+            }
+        }
+        // carried low-vote outliers: (previous high-vote outlier, p) in raster order
+        const int k0 = r > 0 ? out_pos[hi_list[r - 1]] + 1 : 0;
+        const int k1 = out_pos[p];
+        for (int k = k0 + lane; k < k1; k += 64) {
+            const int qp = out_list[k];
+            const int c = vote[qp];
+            const uint16_t* s = samples + (size_t)qp * kMaxSamples;
+            for (int m = 0; m < c; ++m) atomicAdd(&hist[s[m]], 1);
+        }
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+        // first maximum: key = (~count, d) minimum
+        uint64_t best = ~0ull;
+        for (int d = lane; d < L; d += 64) {
+            const uint64_t key = ((uint64_t)(0xffffffffu - (uint32_t)hist[d]) << 32) | (uint32_t)d;
+            best = key < best ? key : best;
+        }
+        best = wave_min_u64(best);
+        const int cmax = (int)(0xffffffffu - (uint32_t)(best >> 32));
+        const int dbest = (int)(uint32_t)best;
+        const int v = vote[p];
+        const float ratio = cmax / (float)v;
+        if (lane == 0) dtmp[p] = ratio > P.voting_ratio && cmax > 0 ? dbest + minD : disp[p];
+        __builtin_amdgcn_wave_barrier();
+    }
+}
+
+// ---------------------------------------------------------------------------
+// proper interpolation
+// ---------------------------------------------------------------------------
+__global__ void k_interp(const int32_t* __restrict__ disp, int32_t* __restrict__ out,
+                         const uint32_t* __restrict__ img0, DevParams P) {
+    const int x = blockIdx.x * blockDim.x + threadIdx.x;
+    const int y = blockIdx.y;
+    const int H = P.H, W = P.W, minD = P.minD;
+    if (x >= W) return;
+    const size_t idx = (size_t)y * W + x;
+    const int cur = disp[idx];
+    if (cur >= minD) { out[idx] = cur; return; }
+    const int dWt[16] = {0, 2, 2, 2, 0, -2, -2, -2, 1, 2, 2, 1, -1, -2, -2, -1};
+    const int dHt[16] = {2, 2, 0, -2, -2, -2, 0, 2, 2, 1, -1, -2, -2, -1, 1, 2};
+    int nd[16], ndiff[16];
+    const uint32_t c0 = img0[idx];
+    for (int dir = 0; dir < 16; ++dir) {
+        nd[dir] = cur;
+        ndiff[dir] = -1;
+        int hD = y, wD = x;
+        bool inside = true, got = false;
+        for (int s = 0; s < P.max_search_depth && inside && !got; ++s) {
+            if (s % 2 == 0) { hD += dHt[dir] / 2; wD += dWt[dir] / 2; }
+            else { hD += dHt[dir] - dHt[dir] / 2; wD += dWt[dir] - dWt[dir] / 2; }
+            inside = hD >= 0 && hD < H && wD >= 0 && wD < W;
+            if (inside) {
+                const int dv = disp[(size_t)hD * W + wD];
+                if (dv >= minD) {
+                    nd[dir] = dv;
+                    ndiff[dir] = color_diff(P, c0, img0[(size_t)hD * W + wD]);
+                    got = true;
+                }
+            }
+        }
+    }
+    int res;
+    if (cur == minD - 1) { // occlusion (:1209)
+        res = nd[0];
+        for (int k = 1; k < 16; ++k) res = min(res, nd[k]);
+    } else {
+        int md = nd[0], mdiff = ndiff[0];
+        for (int k = 1; k < 16; ++k) {
+            if (mdiff < 0 || (mdiff > ndiff[k] && ndiff[k] > 0)) { md = nd[k]; mdiff = ndiff[k]; }
+        }
+        res = md;
+    }
+    out[idx] = res;
+}
+
+// ---------------------------------------------------------------------------
+// discontinuity adjustment: gray -> equalizeHist -> blur -> Canny -> adjust
+// ---------------------------------------------------------------------------
+__global__ void k_gray_hist(const int32_t* __restrict__ disp, uint8_t* __restrict__ gray,
+                            int32_t* __restrict__ hist, int n) {
+    __shared__ int h[256];
+    h[threadIdx.x] = 0;
+    __syncthreads();
+    for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
+        const int d = disp[i];
+        const uint8_t g = d < 0 ? 0 : (uint8_t)d; // (uchar) wraps > 255 (:1249)
+        gray[i] = g;
+        atomicAdd(&h[g], 1);
+    }
+    __syncthreads();
+    if (h[threadIdx.x]) atomicAdd(&hist[threadIdx.x], h[threadIdx.x]);
+}
+
+__device__ __forceinline__ int reflect101(int i, int n) {
+    if (n == 1) return 0;
+    if (i < 0) i = -i;
+    if (i >= n) i = 2 * n - 2 - i;
+    return i;
+}
+
+// equalizeHist LUT (imgproc histogram.cpp): lut[i] = saturate_cast<uchar>(sum * scale),
+// scale = 255.f / (total - hist[first nonzero]); one wave, serial 256-entry prefix.
+__global__ void k_eq_lut(const int32_t* __restrict__ hist, uint8_t* __restrict__ lut_out, int total) {
+    if (threadIdx.x != 0) return;
+    uint8_t* lut = lut_out;
+    int i = 0;
+    while (i < 256 && hist[i] == 0) ++i;
+    for (int k = 0; k < 256; ++k) lut[k] = 0;
+    if (i < 256) {
+        if (hist[i] == total) {
+            lut[i] = (uint8_t)i;
+        } else {
+            const float scale = (256 - 1.f) / (float)(total - hist[i]);
+            int sum = 0;
+            for (int k = i + 1; k < 256; ++k) {
+                sum += hist[k];
+                const int v = (int)rintf((float)sum * scale);
+                lut[k] = (uint8_t)(v < 0 ? 0 : (v > 255 ? 255 : v));
+            }
+        }
+    }
+}
+
+// blur 3x3 BORDER_REFLECT_101 of the equalised map with the ColumnSum<ushort,uchar>
+// fixed-point divide ((s+4)*932068)>>23 == round(s/9).
+__global__ void k_eq_blur(const uint8_t* __restrict__ gray, const uint8_t* __restrict__ lut_g,
+                          uint8_t* __restrict__ eq_out, uint8_t* __restrict__ blurred, int H, int W) {
+    __shared__ uint8_t lut[256];
+    lut[threadIdx.x] = lut_g[threadIdx.x];
+    __syncthreads();
+    const int x = blockIdx.x * blockDim.x + threadIdx.x;
+    const int y = blockIdx.y;
+    if (x >= W) return;
+    int s = 0;
+    for (int dy = -1; dy <= 1; ++dy) {
+        const int yy = reflect101(y + dy, H);
+        for (int dx = -1; dx <= 1; ++dx) s += lut[gray[(size_t)yy * W + reflect101(x + dx, W)]];
+    }
+    blurred[(size_t)y * W + x] = (uint8_t)(((s + 4) * 932068) >> 23);
+    if (eq_out) eq_out[(size_t)y * W + x] = lut[gray[(size_t)y * W + x]];
+}
+
+// Sobel 3x3 (BORDER_REPLICATE) -> dx, dy (CV_16S), L1 magnitude.
+__global__ void k_sobel(const uint8_t* __restrict__ src, int16_t* __restrict__ dx,
+                        int16_t* __restrict__ dy, int32_t* __restrict__ mag, int H, int W) {
+    const int x = blockIdx.x * blockDim.x + threadIdx.x;
+    const int y = blockIdx.y;
+    if (x >= W) return;
+    auto S = [&](int yy, int xx) -> int {
+        yy = yy < 0 ? 0 : (yy >= H ? H - 1 : yy);
+        xx = xx < 0 ? 0 : (xx >= W ? W - 1 : xx);
+        return src[(size_t)yy * W + xx];
+    };
+    const int gx = (S(y - 1, x + 1) + 2 * S(y, x + 1) + S(y + 1, x + 1)) -
+                   (S(y - 1, x - 1) + 2 * S(y, x - 1) + S(y + 1, x - 1));
+    const int gy = (S(y + 1, x - 1) + 2 * S(y + 1, x) + S(y + 1, x + 1)) -
+                   (S(y - 1, x - 1) + 2 * S(y - 1, x) + S(y - 1, x + 1));
+    const size_t i = (size_t)y * W + x;
+    dx[i] = (int16_t)gx;
+    dy[i] = (int16_t)gy;
+    mag[i] = abs(gx) + abs(gy);
+}
+
+// Non-maximum suppression (canny.cpp TG22 fixed point, zero magnitude outside the image).
+// map: 1 = not an edge, 0 = weak candidate, 2 = strong (m > high).
+__global__ void k_nms(const int16_t* __restrict__ dx, const int16_t* __restrict__ dy,
+                      const int32_t* __restrict__ mag, uint8_t* __restrict__ map, int H, int W,
+                      int low, int high) {
+    const int x = blockIdx.x * blockDim.x + threadIdx.x;
+    const int y = blockIdx.y;
+    if (x >= W) return;
+    auto M = [&](int yy, int xx) -> int {
+        if (yy < 0 || yy >= H || xx < 0 || xx >= W) return 0;
+        return mag[(size_t)yy * W + xx];
+    };
+    const size_t i = (size_t)y * W + x;
+    const int m = mag[i];
+    bool keep = false;
+    if (m > low) {
+        const int xs = dx[i], ys = dy[i];
+        const int ax = abs(xs);
+        const int ay = abs(ys) << 15;
+        const int tg22x = ax * 13573; // (int)(0.4142135623730950488 * (1 << 15) + 0.5)
+        if (ay < tg22x) {
+            keep = m > M(y, x - 1) && m >= M(y, x + 1);
+        } else {
+            const int tg67x = tg22x + (ax << 16);
+            if (ay > tg67x) {
+                keep = m > M(y - 1, x) && m >= M(y + 1, x);
+            } else {
+                const int s = (xs ^ ys) < 0 ? -1 : 1;
+                keep = m > M(y - 1, x - s) && m > M(y + 1, x + s);
+            }
+        }
+    }
+    map[i] = !keep ? 1 : (m > high ? 2 : 0);
+}
+
+// Hysteresis = 8-connected components of {map != 1} containing a strong pixel.
+// Lock-free union-find: links always point to the smaller index (no cycles); a root is
+// re-linked only by CAS, so stale reads just cost a retry.
+__device__ __forceinline__ int uf_find(int* parent, int x) {
+    int p = __hip_atomic_load(&parent[x], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    while (p != x) {
+        x = p;
+        p = __hip_atomic_load(&parent[x], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    return x;
+}
+__device__ __forceinline__ void uf_union(int* parent, int a, int b) {
+    while (true) {
+        a = uf_find(parent, a);
+        b = uf_find(parent, b);
+        if (a == b) return;
+        if (a < b) { const int t = a; a = b; b = t; }
+        const int old = atomicCAS(&parent[a], a, b);
+        if (old == a) return;
+        a = old;
+    }
+}
+
+__global__ void k_uf_init(const uint8_t* __restrict__ map, int32_t* __restrict__ label, int n) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) label[i] = map[i] != 1 ? i : -1;
+}
+
+__global__ void k_uf_merge(const uint8_t* __restrict__ map, int32_t* __restrict__ label, int H, int W) {
+    const int x = blockIdx.x * blockDim.x + threadIdx.x;
+    const int y = blockIdx.y;
+    if (x >= W) return;
+    const int i = y * W + x;
+    if (map[i] == 1) return;
+    // W, NW, N, NE neighbours cover every 8-connected edge once
+    if (x > 0 && map[i - 1] != 1) uf_union(label, i, i - 1);
+    if (y > 0) {
+        if (x > 0 && map[i - W - 1] != 1) uf_union(label, i, i - W - 1);
+        if (map[i - W] != 1) uf_union(label, i, i - W);
+        if (x + 1 < W && map[i - W + 1] != 1) uf_union(label, i, i - W + 1);
+    }
+}
+
+__global__ void k_uf_flatten_mark(const uint8_t* __restrict__ map, int32_t* __restrict__ label,
+                                  uint8_t* __restrict__ strong, int n) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n || map[i] == 1) return;
+    int r = i;
+    while (label[r] != r) r = label[r];
+    label[i] = r;
+    if (map[i] == 2) strong[r] = 1;
+}
+
+__global__ void k_uf_final(const uint8_t* __restrict__ map, const int32_t* __restrict__ label,
+                           const uint8_t* __restrict__ strong, uint8_t* __restrict__ edges, int n) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    edges[i] = (map[i] != 1 && strong[label[i]]) ? 255 : 0;
+}
+
+// discontinuityAdjustment body (:1266-1339); reads the pre-adjust map, writes dtmp.
+__global__ void k_adjust(const int32_t* __restrict__ disp, int32_t* __restrict__ out,
+                         const uint8_t* __restrict__ edges, const float* __restrict__ vol0,
+                         DevParams P) {
+    const int x = blockIdx.x * blockDim.x + threadIdx.x;
+    const int y = blockIdx.y;
+    const int H = P.H, W = P.W, minD = P.minD, Lp = P.Lp;
+    if (x >= W) return;
+    const size_t i = (size_t)y * W + x;
+    int res = disp[i];
+    if (y >= 1 && y < H - 1 && x >= 1 && x < W - 1 && edges[i]) {
+        auto E = [&](int yy, int xx) -> bool { return edges[(size_t)yy * W + xx] != 0; };
+        int direction = -1;
+        if (E(y - 1, x - 1) && E(y + 1, x + 1)) direction = 0;
+        else if (E(y - 1, x + 1) && E(y + 1, x - 1)) direction = 4;
+        else if (E(y - 1, x) || E(y + 1, x)) {
+            if (E(y - 1, x - 1) || E(y - 1, x) || E(y - 1, x + 1))
+                if (E(y + 1, x - 1) || E(y + 1, x) || E(y + 1, x + 1)) direction = 2;
+        } else {
+            if (E(y - 1, x - 1) || E(y, x - 1) || E(y + 1, x - 1))
+                if (E(y - 1, x + 1) || E(y, x + 1) || E(y + 1, x + 1)) direction = 6;
+        }
+        if (direction != -1) {
+            const int dHt[8] = {-1, 1, -1, 1, -1, 1, 0, 0};
+            const int dWt[8] = {-1, 1, 0, 0, 1, -1, -1, 1};
+            int dsel = res;
+            direction = (direction + 4) % 8;
+            if (dsel >= minD) {
+                float cost = vol0[i * Lp + (dsel - minD)];
+                const int y1 = y + dHt[direction], x1 = x + dWt[direction];
+                const int y2 = y + dHt[direction + 1], x2 = x + dWt[direction + 1];
+                const size_t i1 = (size_t)y1 * W + x1, i2 = (size_t)y2 * W + x2;
+                const int d1 = disp[i1], d2 = disp[i2];
+                const float cost1 = d1 >= minD ? vol0[i1 * Lp + (d1 - minD)] : -1.f;
+                const float cost2 = d2 >= minD ? vol0[i2 * Lp + (d2 - minD)] : -1.f;
+                if (cost1 != -1.f && cost1 < cost) { dsel = d1; cost = cost1; }
+                if (cost2 != -1.f && cost2 < cost) { dsel = d2; }
+            }
+            res = dsel;
+        }
+    }
+    out[i] = res;
+}
+
+// subpixelEnhancement (:1344-1370)
+__global__ void k_subpix(const int32_t* __restrict__ disp, const float* __restrict__ vol0,
+                         float* __restrict__ sub, DevParams P) {
+    const int x = blockIdx.x * blockDim.x + threadIdx.x;
+    const int y = blockIdx.y;
+    const int W = P.W, minD = P.minD, Lp = P.Lp;
+    if (x >= W) return;
+    const size_t i = (size_t)y * W + x;
+    const int d = disp[i];
+    float inter = (float)d;
+    if (d > P.minD && d < P.maxD) {
+        const float* c = vol0 + i * Lp;
+        const float c0 = c[d - minD], cp = c[d + 1 - minD], cm = c[d - 1 - minD];
+        const float diff = (cp - cm) / (2 * (cp + cm - 2 * c0));
+        if (diff > -1 && diff < 1) inter -= diff;
+    }
+    sub[i] = inter;
+}
+
+__device__ __forceinline__ void sort2(float& a, float& b) {
+    const float lo = fminf(a, b), hi = fmaxf(a, b);
+    a = lo;
+    b = hi;
+}
+
+// medianBlur 3x3 CV_32F (BORDER_REPLICATE) + ROI/mask post-processing (:388-403) + store.
+__global__ void k_median_out(const float* __restrict__ sub, float* __restrict__ out,
+                             size_t out_step, const uint32_t* __restrict__ orig_left,
+                             int roi_or_mask, int offset, int H, int W) {
+    const int x = blockIdx.x * blockDim.x + threadIdx.x;
+    const int y = blockIdx.y;
+    if (x >= W) return;
+    float v[9];
+    int k = 0;
+    for (int dy = -1; dy <= 1; ++dy) {
+        const int yy = min(max(y + dy, 0), H - 1);
+        for (int dx = -1; dx <= 1; ++dx) v[k++] = sub[(size_t)yy * W + min(max(x + dx, 0), W - 1)];
+    }
+    // odd-even transposition network: exact selection of the median (no arithmetic)
+#pragma unroll
+    for (int r = 0; r < 9; ++r) {
+#pragma unroll
+        for (int i = (r & 1); i + 1 < 9; i += 2) sort2(v[i], v[i + 1]);
+    }
+    float d = v[4];
+    if (roi_or_mask) {
+        if (d > 0) d = d + offset;                              // disparityOffset :1415-1427
+        if ((orig_left[(size_t)y * W + x] == 0 && d > 0) || d == 0) d = -1.f;
+    }
+    *reinterpret_cast<float*>(reinterpret_cast<char*>(out) + (size_t)y * out_step + (size_t)x * 4) = d;
+}
+
+// ---------------------------------------------------------------------------
+// debug layout conversions
+// ---------------------------------------------------------------------------
+__global__ void k_vol_to_ref(const float* __restrict__ vol, float* __restrict__ ref, DevParams P) {
+    const size_t N = (size_t)P.H * P.W;
+    const int v = blockIdx.z;
+    const int d = blockIdx.y;
+    for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < N; i += (size_t)gridDim.x * blockDim.x)
+        ref[((size_t)v * P.L + d) * N + i] = vol[((size_t)v * N + i) * P.Lp + d];
+}
+
+__global__ void k_arms_to_ref(const uint32_t* __restrict__ arms, int32_t* __restrict__ ref, DevParams P) {
+    const size_t N = (size_t)P.H * P.W;
+    const int v = blockIdx.y;
+    for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < N; i += (size_t)gridDim.x * blockDim.x) {
+        const uint32_t a = arms[(size_t)v * N + i];
+        for (int k = 0; k < 4; ++k) ref[((size_t)v * 4 + k) * N + i] = (a >> (8 * k)) & 0xff;
+    }
+}
+
+// ---------------------------------------------------------------------------
+// launchers
+// ---------------------------------------------------------------------------
+size_t refine_scan_blocks(int n) { return (size_t)(n + SC_BLOCK - 1) / SC_BLOCK; }
+
+static dim3 grid2d(int W, int H, int bx) { return dim3((W + bx - 1) / bx, H); }
+
+void launch_outlier(const RefineBufs& B, const DevParams& P, hipStream_t st) {
+    hipLaunchKernelGGL(k_outlier, grid2d(P.W, P.H, 256), dim3(256), 0, st, B.disp0, B.disp1, B.dm, P);
+}
+
+void launch_region_voting(const RefineBufs& B, const uint32_t* arms0, int hf, const DevParams& P,
+                          hipStream_t st) {
+    const int n = P.H * P.W;
+    const int nb = (int)refine_scan_blocks(n);
+    hipLaunchKernelGGL(k_vote_count, grid2d(P.W, P.H, 128), dim3(128), 0, st, B.dm, arms0, B.vote,
+                       B.samples, B.flags, hf, P);
+    hipLaunchKernelGGL(k_scan_count, dim3(nb), dim3(SC_THREADS), 0, st, B.flags, n, B.bsum);
+    hipLaunchKernelGGL(k_scan_blocks, dim3(1), dim3(SC_THREADS), 0, st, B.bsum, nb, B.counts);
+    hipLaunchKernelGGL(k_scan_scatter, dim3(nb), dim3(SC_THREADS), 0, st, B.flags, n, B.bsum,
+                       B.out_pos, B.out_list, B.hi_list);
+    hipMemcpyAsync(B.dtmp, B.dm, (size_t)n * sizeof(int32_t), hipMemcpyDeviceToDevice, st);
+    const size_t lds = (size_t)(VD_THREADS / 64) * P.L * sizeof(int);
+    hipLaunchKernelGGL(k_vote_decide, dim3(1024), dim3(VD_THREADS), lds, st, B.dm, B.dtmp, arms0,
+                       B.vote, B.samples, B.out_pos, B.out_list, B.hi_list, B.counts, hf, P);
+    hipMemcpyAsync(B.dm, B.dtmp, (size_t)n * sizeof(int32_t), hipMemcpyDeviceToDevice, st);
+}
+
+void launch_interpolation(const RefineBufs& B, const uint32_t* img0, const DevParams& P,
+                          hipStream_t st) {
+    const size_t n = (size_t)P.H * P.W;
+    hipLaunchKernelGGL(k_interp, grid2d(P.W, P.H, 128), dim3(128), 0, st, B.dm, B.dtmp, img0, P);
+    hipMemcpyAsync(B.dm, B.dtmp, n * sizeof(int32_t), hipMemcpyDeviceToDevice, st);
+}
+
+void launch_discontinuity(const RefineBufs& B, const float* vol0, const DevParams& P,
+                          hipStream_t st) {
+    const int n = P.H * P.W;
+    hipMemsetAsync(B.hist, 0, 256 * sizeof(int32_t), st);
+    hipLaunchKernelGGL(k_gray_hist, dim3(min((n + 255) / 256, 1024)), dim3(256), 0, st, B.dm, B.gray, B.hist, n);
+    uint8_t* lut = reinterpret_cast<uint8_t*>(B.hist + 256);
+    hipLaunchKernelGGL(k_eq_lut, dim3(1), dim3(64), 0, st, B.hist, lut, n);
+    hipLaunchKernelGGL(k_eq_blur, grid2d(P.W, P.H, 256), dim3(256), 0, st, B.gray, lut,
+                       B.gray_eq, B.blurred, P.H, P.W);
+    hipLaunchKernelGGL(k_sobel, grid2d(P.W, P.H, 256), dim3(256), 0, st, B.blurred, B.dx, B.dy, B.mag, P.H, P.W);
+    hipLaunchKernelGGL(k_nms, grid2d(P.W, P.H, 256), dim3(256), 0, st, B.dx, B.dy, B.mag, B.map,
+                       P.H, P.W, P.canny_low, P.canny_high);
+    hipLaunchKernelGGL(k_uf_init, dim3((n + 255) / 256), dim3(256), 0, st, B.map, B.label, n);
+    hipLaunchKernelGGL(k_uf_merge, grid2d(P.W, P.H, 256), dim3(256), 0, st, B.map, B.label, P.H, P.W);
+    hipMemsetAsync(B.strong, 0, (size_t)n, st);
+    hipLaunchKernelGGL(k_uf_flatten_mark, dim3((n + 255) / 256), dim3(256), 0, st, B.map, B.label, B.strong, n);
+    hipLaunchKernelGGL(k_uf_final, dim3((n + 255) / 256), dim3(256), 0, st, B.map, B.label, B.strong, B.edges, n);
+    hipLaunchKernelGGL(k_adjust, grid2d(P.W, P.H, 256), dim3(256), 0, st, B.dm, B.dtmp, B.edges, vol0, P);
+    hipMemcpyAsync(B.dm, B.dtmp, (size_t)n * sizeof(int32_t), hipMemcpyDeviceToDevice, st);
+}
+
+void launch_subpixel_median(const RefineBufs& B, const float* vol0, const uint32_t* orig_left,
+                            float* out, size_t out_step, int roi_or_mask, int offset,
+                            const DevParams& P, hipStream_t st) {
+    hipLaunchKernelGGL(k_subpix, grid2d(P.W, P.H, 256), dim3(256), 0, st, B.dm, vol0, B.subpix, P);
+    hipLaunchKernelGGL(k_median_out, grid2d(P.W, P.H, 256), dim3(256), 0, st, B.subpix, out,
+                       out_step, orig_left, roi_or_mask, offset, P.H, P.W);
+}
+
+void launch_vol_to_ref(const float* vol, float* ref, int views, const DevParams& P, hipStream_t st) {
+    hipLaunchKernelGGL(k_vol_to_ref, dim3(256, P.L, views), dim3(256), 0, st, vol, ref, P);
+}
+
+void launch_arms_to_ref(const uint32_t* arms, int32_t* ref, const DevParams& P, hipStream_t st) {
+    hipLaunchKernelGGL(k_arms_to_ref, dim3(256, 2), dim3(256), 0, st, arms, ref, P);
+}
+
+}  // namespace tsm

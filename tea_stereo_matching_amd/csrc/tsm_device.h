@@ -1,0 +1,112 @@
+// tsm_device.h -- shared device-side definitions for the gfx950 AD-Census kernels.
+//
+// HBM layout of one pair's workspace (see DESIGN.md "Data layout"):
+//   img   [2][H][W]      u32  packed B|G<<8|R<<16 of the matched view images
+//   desc  [2][H][W][12]  u32  ternary census descriptors (gt/lt bit planes)
+//   vol   [2][H][W][Lp]  f32  pixel-major cost volume, Lp = round_up(L, 4)
+//   arms  [2][H][W]      u32  packed u8 arms: up | down<<8 | left<<16 | right<<24
+//   ws    [2][2][H][W]   i32  cross-window sizes (horizontal-first, vertical-first)
+// Pixel-major volumes make every per-pixel L-vector one contiguous 16-B-aligned run:
+// a wave owns a pixel, lanes own 4 consecutive disparities (float4), so arm lengths,
+// scanline minima and WTA are wave-uniform / wave reductions with no divergence.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace tsm {
+
+constexpr int kWave = 64;
+
+// POD kernel parameters (ADCensusParams, stereo_utils.h:209-244, plus geometry).
+struct DevParams {
+    int H, W;          // image size
+    int L, Lp;         // labels (max-min+1) and padded vector length (multiple of 4)
+    int minD, maxD;    // disparity range (inclusive)
+    int color_model;   // 0 RGB, 1 HSI
+    int mask;          // mask matching
+    int censusW, censusH;
+    int color_thresh1, color_thresh2;
+    int sat_thresh1, sat_thresh2;
+    int int_thresh1, int_thresh2;
+    int max_length1, max_length2;
+    int color_diff;
+    float pi1, pi2;
+    float p1t[3], p2t[3]; // P1/P2 by #similar (d1<colorDiff)+(d2<colorDiff): /10, /4, x1 (ADCensus.cpp:954-979)
+    int disp_tolerance;
+    int voting_thresh;
+    float voting_ratio;
+    int max_search_depth;
+    int canny_low, canny_high;
+    int omp_threads;   // scanline race emulation (0/1 = serial semantics)
+};
+
+__device__ __forceinline__ int iabs_(int x) { return x < 0 ? -x : x; }
+__device__ __forceinline__ int ch(uint32_t p, int c) { return (p >> (8 * c)) & 0xff; }
+
+// colorDiff, ADCensus.cpp:583-602.
+__device__ __forceinline__ int color_diff(const DevParams& P, uint32_t a, uint32_t b) {
+    if (P.color_model == 0) {
+        int d0 = iabs_(ch(a, 0) - ch(b, 0));
+        int d1 = iabs_(ch(a, 1) - ch(b, 1));
+        int d2 = iabs_(ch(a, 2) - ch(b, 2));
+        return max(d0, max(d1, d2));
+    }
+    int hd = iabs_(ch(a, 0) - ch(b, 0));
+    return min(hd, 255 - hd);
+}
+
+// DPP move with an `old` fallback for lanes whose source is out of range.
+template <int CTRL>
+__device__ __forceinline__ float dpp_f(float v, float old) {
+    return __int_as_float(__builtin_amdgcn_update_dpp(__float_as_int(old), __float_as_int(v), CTRL,
+                                                      0xF, 0xF, false));
+}
+template <int CTRL>
+__device__ __forceinline__ uint32_t dpp_u(uint32_t v, uint32_t old) {
+    return (uint32_t)__builtin_amdgcn_update_dpp((int)old, (int)v, CTRL, 0xF, 0xF, false);
+}
+
+constexpr int DPP_QUAD_1032 = 0xB1;     // quad_perm [1,0,3,2]
+constexpr int DPP_QUAD_2301 = 0x4E;     // quad_perm [2,3,0,1]
+constexpr int DPP_ROW_MIRROR = 0x140;
+constexpr int DPP_ROW_HALF_MIRROR = 0x141;
+constexpr int DPP_WAVE_SHL1 = 0x130;    // lane l <- lane l+1
+constexpr int DPP_WAVE_SHR1 = 0x138;    // lane l <- lane l-1
+
+// Wave-wide min of NON-NEGATIVE floats (cost values), result uniform in every lane.
+// Non-negative IEEE floats order like their bit patterns, so the cross-row step runs
+// on the scalar unit as unsigned integer min.
+__device__ __forceinline__ float wave_min_nonneg(float v) {
+    const float inf = __int_as_float(0x7f800000);
+    v = fminf(v, dpp_f<DPP_QUAD_1032>(v, inf));
+    v = fminf(v, dpp_f<DPP_QUAD_2301>(v, inf));
+    v = fminf(v, dpp_f<DPP_ROW_HALF_MIRROR>(v, inf));
+    v = fminf(v, dpp_f<DPP_ROW_MIRROR>(v, inf));
+    uint32_t r0 = __builtin_amdgcn_readlane(__float_as_uint(v), 0);
+    uint32_t r1 = __builtin_amdgcn_readlane(__float_as_uint(v), 16);
+    uint32_t r2 = __builtin_amdgcn_readlane(__float_as_uint(v), 32);
+    uint32_t r3 = __builtin_amdgcn_readlane(__float_as_uint(v), 48);
+    uint32_t m = min(min(r0, r1), min(r2, r3));
+    return __uint_as_float(m);
+}
+
+// Wave-wide min of u64 keys (e.g. (float_bits << 32) | d for WTA first-min).
+__device__ __forceinline__ uint64_t wave_min_u64(uint64_t v) {
+    for (int off = 32; off >= 1; off >>= 1) {
+        uint32_t lo = (uint32_t)v, hi = (uint32_t)(v >> 32);
+        uint32_t olo = (uint32_t)__shfl_xor((int)lo, off);
+        uint32_t ohi = (uint32_t)__shfl_xor((int)hi, off);
+        uint64_t o = ((uint64_t)ohi << 32) | olo;
+        v = o < v ? o : v;
+    }
+    return v;
+}
+
+__device__ __forceinline__ int wave_sum_i(int v) {
+    for (int off = 32; off >= 1; off >>= 1) v += __shfl_xor(v, off);
+    return v;
+}
+
+__device__ __forceinline__ int lane_id() { return threadIdx.x & 63; }
+
+}  // namespace tsm

@@ -1,0 +1,80 @@
+// tsm_launch.h -- host-side launchers of the gfx950 kernels (one per .hip file), called
+// by the engine.  Each .hip file owns its kernels; no relocatable device code needed.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "tsm_device.h"
+
+namespace tsm {
+
+// k_cost.hip
+void launch_pack(const uint8_t* left, const uint8_t* right, size_t step, int H, int W,
+                 uint32_t* img, hipStream_t st);
+void launch_hsi(const uint32_t* src, uint32_t* tmp, uint32_t* dst, int H, int W, int filter,
+                hipStream_t st);
+void launch_census(const uint32_t* img, uint32_t* desc, const DevParams& P, hipStream_t st);
+size_t cost_volume_lds_bytes(const DevParams& P, int lutA_n);
+int launch_cost_volume(const uint32_t* img, const uint32_t* desc, const float* lutA, int lutA_n,
+                       const float* lutB, float* vol, const DevParams& P, hipStream_t st);
+
+// k_aggregate.hip
+void launch_arms(const uint32_t* img, uint32_t* arms, const DevParams& P, hipStream_t st);
+void launch_window_sizes(const uint32_t* arms, int32_t* ws, const DevParams& P, hipStream_t st);
+void launch_color_grad(const uint32_t* img, uint8_t* gv, uint8_t* gh, const DevParams& P,
+                       hipStream_t st);
+size_t agg_lds_bytes(const DevParams& P);
+int launch_agg_line(float* vol, const uint32_t* arms, const int32_t* ws, int horizontal,
+                    const DevParams& P, hipStream_t st);
+
+// k_scanline.hip
+int launch_scan_vertical(float* vol, const uint8_t* gv, const uint32_t* img, int dir,
+                         const DevParams& P, hipStream_t st);
+int launch_scan_horizontal(float* vol, const uint8_t* gh, const uint32_t* img, int dir,
+                           int32_t* wta, int store_view1, const DevParams& P, hipStream_t st);
+
+// k_refine.hip
+struct RefineBufs {
+    int32_t* disp0;   // WTA view 0           [H][W]
+    int32_t* disp1;   // WTA view 1           [H][W]
+    int32_t* dm;      // working disparity    [H][W]
+    int32_t* dtmp;    // Jacobi scratch       [H][W]
+    int32_t* vote;    // per-pixel vote count [H][W]
+    uint16_t* samples;// [H][W][20] low-vote samples
+    uint8_t* flags;   // [H][W]
+    int32_t* out_pos; // [H][W]
+    int32_t* out_list;// [H][W]
+    int32_t* hi_list; // [H][W]
+    int32_t* bsum;    // scan block sums [2 * nblocks]
+    int32_t* counts;  // [4]
+    uint8_t* gray;    // [H][W]
+    int32_t* hist;    // [256] + 64 ints of LUT scratch
+    uint8_t* gray_eq; // [H][W] equalised gray (debug dump)
+    uint8_t* blurred; // [H][W]
+    int16_t* dx;      // [H][W]
+    int16_t* dy;      // [H][W]
+    int32_t* mag;     // [H][W]
+    uint8_t* map;     // [H][W]
+    int32_t* label;   // [H][W]
+    uint8_t* strong;  // [H][W]
+    uint8_t* edges;   // [H][W]
+    float* subpix;    // [H][W]
+};
+size_t refine_scan_blocks(int n);
+void launch_outlier(const RefineBufs& B, const DevParams& P, hipStream_t st);
+void launch_region_voting(const RefineBufs& B, const uint32_t* arms0, int horizontal_first,
+                          const DevParams& P, hipStream_t st);
+void launch_interpolation(const RefineBufs& B, const uint32_t* img0, const DevParams& P,
+                          hipStream_t st);
+void launch_discontinuity(const RefineBufs& B, const float* vol0, const DevParams& P,
+                          hipStream_t st);
+void launch_subpixel_median(const RefineBufs& B, const float* vol0, const uint32_t* orig_left,
+                            float* out, size_t out_step, int roi_or_mask, int offset,
+                            const DevParams& P, hipStream_t st);
+
+// debug helpers
+void launch_vol_to_ref(const float* vol, float* ref, int views, const DevParams& P,
+                       hipStream_t st);
+void launch_arms_to_ref(const uint32_t* arms, int32_t* ref, const DevParams& P, hipStream_t st);
+
+}  // namespace tsm

@@ -1,0 +1,195 @@
+"""HIP path vs the oracle (CPU restatement of source/ADCensus.cpp), on a real MI355X.
+
+Bar: bit-exact.  Census, arms, WTA/outlier/voting/interpolation maps are integers; the
+cost volumes are fp32 computed in the reference's exact operation order (sequential arm
+sums, host-built expf tables, no FMA contraction), so every stage is compared with
+np.array_equal -- including the final float disparity.
+"""
+import os
+
+import numpy as np
+import pytest
+
+from conftest import GOLDEN, host_threads, load_bgr
+
+pytestmark = pytest.mark.gpu
+
+STAGES = ("images", "cost_init", "arms", "cost_agg", "cost_scan", "wta", "outlier", "voting",
+          "interp", "gray", "edges", "adjusted", "subpix")
+
+
+@pytest.fixture(scope="module")
+def tsm():
+    import tea_stereo_matching_amd as T
+
+    if T.device_count() == 0:
+        pytest.fail("no HIP device visible to a -m gpu test")
+    return T
+
+
+@pytest.fixture(scope="module")
+def matcher(tsm):
+    m = tsm.ADCensus(0)
+    yield m
+    m.close()
+
+
+def _oracle_params(oracle, model, mn, mx, **kw):
+    return oracle.default_params(model, mn, mx, num_threads=host_threads(), **kw)
+
+
+def _gpu(matcher, tsm, left, right, model, mn, mx, stages=(), omp=0, roi=False, mask=False):
+    matcher.setMatchingStrategy(tsm.ColorModel(model), roi, mask)
+    matcher.setMinMaxDisparity(mn, mx)
+    matcher.setOmpEmulation(omp)
+    if stages:
+        return matcher.compute_debug(left, right, stages)
+    return matcher.compute(left, right), {}
+
+
+def _assert_stages_equal(g, o, stages):
+    for s in stages:
+        a, b = g[s], o[s]
+        if s == "cost_scan":  # the GPU keeps both views only in debug runs; compare both
+            pass
+        if not np.array_equal(a, b):
+            diff = np.argwhere(a != b) if a.shape == b.shape else None
+            n = 0 if diff is None else len(diff)
+            first = None if diff is None or not n else tuple(diff[0])
+            pytest.fail(f"stage {s}: {n} mismatches (shape {a.shape} vs {b.shape}), first at {first}"
+                        + ("" if first is None else f": gpu={a[first]} oracle={b[first]}"))
+
+
+def _synthetic(tsm, seed, H, W, L):
+    return tsm.synthetic.make_scene(seed, H, W, L)[:2]
+
+
+CASES = [
+    # (seed, H, W, minD, maxD)
+    (1, 64, 96, 0, 24),
+    (2, 120, 160, 0, 48),
+    (3, 97, 131, 0, 64),     # odd sizes, L=65 (Lp padding)
+    (4, 80, 120, 5, 40),     # minD > 0 (reference index quirks, :556-561, :1398)
+    (5, 48, 64, 0, 40),      # D >= W/2
+]
+
+
+@pytest.mark.parametrize("case", CASES, ids=[f"s{c[0]}_{c[1]}x{c[2]}_d{c[3]}-{c[4]}" for c in CASES])
+def test_stages_bit_exact_synthetic(matcher, tsm, oracle, case):
+    seed, H, W, mn, mx = case
+    left, right = _synthetic(tsm, seed, H, W, mx - mn + 1)
+    d_g, g = _gpu(matcher, tsm, left, right, 0, mn, mx, STAGES)
+    d_o, o = oracle.compute(left, right, _oracle_params(oracle, oracle.RGB, mn, mx), STAGES)
+    _assert_stages_equal(g, o, STAGES)
+    assert np.array_equal(d_g, d_o)
+
+
+def test_stages_bit_exact_demo_crop(matcher, tsm, oracle, demo_pair_0600):
+    l, r = demo_pair_0600
+    left, right = l[300:428, 400:656].copy(), r[300:428, 400:656].copy()
+    d_g, g = _gpu(matcher, tsm, left, right, 0, 0, 64, STAGES)
+    d_o, o = oracle.compute(left, right, _oracle_params(oracle, oracle.RGB, 0, 64), STAGES)
+    _assert_stages_equal(g, o, STAGES)
+    assert np.array_equal(d_g, d_o)
+
+
+def test_uniform_image_early_exit(matcher, tsm, oracle):
+    # flat images: min_k C(q,k) == 0 leaves scanline pixels untouched (:880-881)
+    left = np.full((40, 72, 3), 128, np.uint8)
+    right = left.copy()
+    d_g, g = _gpu(matcher, tsm, left, right, 0, 0, 16, STAGES)
+    d_o, o = oracle.compute(left, right, _oracle_params(oracle, oracle.RGB, 0, 16), STAGES)
+    _assert_stages_equal(g, o, STAGES)
+    assert np.array_equal(d_g, d_o)
+
+
+def test_tiny_image_all_border(matcher, tsm, oracle):
+    # every census window leaves the image -> cost 2.f everywhere (:562-566)
+    rng = np.random.default_rng(7)
+    left = rng.integers(0, 256, (6, 8, 3), dtype=np.uint8)
+    right = rng.integers(0, 256, (6, 8, 3), dtype=np.uint8)
+    d_g, _ = _gpu(matcher, tsm, left, right, 0, 0, 3)
+    d_o, _ = oracle.compute(left, right, _oracle_params(oracle, oracle.RGB, 0, 3))
+    assert np.array_equal(d_g, d_o)
+
+
+def test_random_noise_pair(matcher, tsm, oracle):
+    # many outliers: exercises the voting carry and interpolation heavily
+    rng = np.random.default_rng(11)
+    left = rng.integers(0, 256, (70, 110, 3), dtype=np.uint8)
+    right = rng.integers(0, 256, (70, 110, 3), dtype=np.uint8)
+    d_g, g = _gpu(matcher, tsm, left, right, 0, 0, 30, STAGES)
+    d_o, o = oracle.compute(left, right, _oracle_params(oracle, oracle.RGB, 0, 30), STAGES)
+    _assert_stages_equal(g, o, STAGES)
+    assert np.array_equal(d_g, d_o)
+
+
+def test_omp_emulation_matches_oracle(matcher, tsm, oracle):
+    left, right = _synthetic(tsm, 21, 90, 150, 33)
+    for T in (3, 20):
+        d_g, g = _gpu(matcher, tsm, left, right, 0, 0, 32, ("cost_scan",), omp=T)
+        d_o, o = oracle.compute(left, right, _oracle_params(oracle, oracle.RGB, 0, 32,
+                                                           scan_emulate_threads=T), ("cost_scan",))
+        _assert_stages_equal(g, o, ("cost_scan",))
+        assert np.array_equal(d_g, d_o)
+
+
+def test_reference_fixture_0600_exact(matcher, tsm, oracle, demo_pair_0600):
+    """Full 1280x720, D=[0,192]: with T=20 emulation the GPU output renders to the
+    reference's own demo-output/0600_adcensus.png pixel for pixel."""
+    left, right = demo_pair_0600
+    d_g, _ = _gpu(matcher, tsm, left, right, 0, 0, 192, omp=20)
+    ref = load_bgr(os.path.join(GOLDEN, "demo", "0600_adcensus.png"))
+    col = oracle.apply_colormap(d_g)
+    assert np.array_equal(col, ref), f"{(col != ref).any(-1).sum()} pixels differ"
+
+
+def test_config_b_serial_bit_exact(matcher, tsm, oracle):
+    """The benchmark workload (1242x375, D=[0,192], RGB) at serial semantics."""
+    left, right, gt = tsm.synthetic.config_b(1000)
+    d_g, _ = _gpu(matcher, tsm, left, right, 0, 0, 192)
+    d_o, _ = oracle.compute(left, right, _oracle_params(oracle, oracle.RGB, 0, 192))
+    assert np.array_equal(d_g, d_o)
+    valid = d_o >= 0
+    assert (np.abs(d_g - d_o)[valid] <= 0.5).mean() >= 0.99
+
+
+def test_batch_equals_single(matcher, tsm):
+    pairs = [_synthetic(tsm, 100 + i, 64, 96, 25) for i in range(5)]
+    matcher.setMatchingStrategy(tsm.ColorModel.RGB)
+    matcher.setMinMaxDisparity(0, 24)
+    matcher.setOmpEmulation(0)
+    matcher.setConcurrency(3)
+    outs = matcher.compute_batch([p[0] for p in pairs], [p[1] for p in pairs])
+    for (l, r), o in zip(pairs, outs):
+        assert np.array_equal(o, matcher.compute(l, r))
+
+
+def test_api_errors_match_reference(matcher, tsm):
+    E = tsm.ADCensusError
+    with pytest.raises(E, match=r"^\[ADCensus\] Set MinMaxDisparity error\.$"):
+        matcher.setMinMaxDisparity(-5, 5)
+    with pytest.raises(E, match=r"^\[ADCensus\] Set MinMaxDisparity error\.$"):
+        matcher.setMinMaxDisparity(10, 10)
+    with pytest.raises(E, match=r"^\[ADCensus\] Offset must be positive\.$"):
+        matcher.setOffset(-1)
+    img = np.zeros((16, 16, 3), np.uint8)
+    with pytest.raises(E, match=r"^\[ADCensus\] Image error\.$"):
+        matcher.compute(img, np.zeros((16, 17, 3), np.uint8))
+    with pytest.raises(E, match=r"^\[ADCensus\] Image error\.$"):
+        matcher.compute(None, img)
+    with pytest.raises(E, match=r"^\[ADCensus\] Image error\.$"):
+        matcher.compute(np.zeros((0, 16, 3), np.uint8), np.zeros((0, 16, 3), np.uint8))
+    # a failed setter leaves the previous range in place
+    matcher.setMinMaxDisparity(0, 32)
+    with pytest.raises(E):
+        matcher.setMinMaxDisparity(5, 1)
+    assert matcher.getMinMaxDisparity() == (0, 32)
+
+
+def test_default_state_is_reference_default(tsm):
+    m = tsm.ADCensus(0)
+    assert m.getMinMaxDisparity() == (0, 64)  # ADCensus.cpp:411-412
+    p = m.params()
+    assert (p.color_thresh1, p.max_length1, p.color_diff) == (5, 17, 3)  # HSI set (:413-414)
+    m.close()

@@ -1,0 +1,27 @@
+#!/bin/bash
+# Runs on the GPU box: smoke, GPU parity tests, short bench.  Every GPU step has its own
+# time limit; a fault / abort / segfault / timeout stops the script (no further GPU work).
+set -u
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+mkdir -p gpurun_out
+step() {  # step <name> <timeout-s> <cmd...>
+    local name=$1 t=$2; shift 2
+    echo "== $name: $*"
+    timeout -k 10 "$t" "$@" > "gpurun_out/$name.log" 2>&1
+    local rc=$?
+    echo "== $name rc=$rc"
+    tail -n 25 "gpurun_out/$name.log"
+    # 0 ok, 1 test failures (no fault) -> continue; anything else -> stop
+    if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then echo "STOP after $name (rc=$rc)"; exit $rc; fi
+    return 0
+}
+for s in "$@"; do
+    case $s in
+        smoke) step smoke 300 python3 -c "import __graft_entry__ as g; g.smoke()" ;;
+        tests) step gpu_tests 900 python3 -m pytest tests -x -q -m gpu ;;
+        tests-k) step gpu_tests 900 python3 -m pytest tests -q -m gpu ;;
+        bench) step bench 600 python3 bench.py ;;
+        bench-short) step bench 400 python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline ;;
+        *) echo "unknown step $s"; exit 2 ;;
+    esac
+done
