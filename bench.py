@@ -82,10 +82,9 @@ def main():
     import torch.distributed as dist
 
     import tea_stereo_matching_amd as tsm
+    from tea_stereo_matching_amd import distributed as Dd
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
+    rank, world, local = Dd.world_info()
     if world > 1:
         torch.cuda.set_device(local)
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
@@ -95,10 +94,10 @@ def main():
     H, W, D = args.height, args.width, args.max_disparity
     L = D + 1
     B = args.batch
-    # synthetic inputs: pair i of rank r uses seed 1000 + r*B + i; uploaded once (HBM-resident)
+    # synthetic inputs: global pair g uses seed 1000 + g; uploaded once (HBM-resident)
     lefts, rights = [], []
-    for i in range(B):
-        l, r, _ = tsm.synthetic.make_scene(1000 + rank * B + i, H, W, L)
+    for g in Dd.shard(rank, B):
+        l, r, _ = tsm.synthetic.make_scene(Dd.pair_seed(g), H, W, L)
         lefts.append(torch.from_numpy(l).to(dev))
         rights.append(torch.from_numpy(r).to(dev))
     outs = torch.empty((B, H, W), dtype=torch.float32, device=dev)
@@ -118,7 +117,7 @@ def main():
     def step():
         m.compute_batch_device_ptr(lp, rp, H, W, W * 3, op, W * 4)
         if world > 1 and not args.no_gather:
-            dist.gather(outs, gathered if rank == 0 else None, dst=0)
+            Dd.gather_to_root(outs, rank, world, gathered)
 
     for _ in range(args.warmup):
         step()
@@ -137,10 +136,7 @@ def main():
     elapsed = time.perf_counter() - t0
     m.setProfiling(False)
     stages = m.stageTimes()
-    if world > 1:
-        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
+    elapsed = Dd.max_over_ranks(elapsed, world, dev)
 
     pairs = world * B * args.steps
     value = pairs / elapsed

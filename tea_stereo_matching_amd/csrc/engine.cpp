@@ -10,6 +10,7 @@
 
 #include <cmath>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <string>
 #include <vector>
@@ -18,6 +19,21 @@
 #include "tsm_launch.h"
 
 using namespace tsm;
+
+namespace tsm {
+static int g_trace = -1;
+void trace_point(const char* what, hipStream_t st) {
+    if (g_trace < 0) {
+        const char* e = std::getenv("TSM_TRACE");
+        g_trace = (e && e[0] == '1') ? 1 : 0;
+    }
+    if (!g_trace) return;
+    hipError_t le = hipGetLastError();
+    hipError_t se = hipStreamSynchronize(st);
+    std::fprintf(stderr, "[tsm] %-40s launch=%s sync=%s\n", what, hipGetErrorString(le), hipGetErrorString(se));
+    std::fflush(stderr);
+}
+}  // namespace tsm
 
 namespace {
 
@@ -261,8 +277,8 @@ int ensure_workspace(tsm_adc* h, Workspace* w, int H, int W) {
     A(w->gv, 2 * N);
     A(w->gh, 2 * N);
     RefineBufs& B = w->rb;
-    A(B.disp0, N * 4);
-    A(B.disp1, N * 4);
+    A(B.disp0, 2 * N * 4);  // [2][H][W]: the fused WTA writes view v at disp0 + v*N
+    B.disp1 = B.disp0 + N;
     A(B.dm, N * 4);
     A(B.dtmp, N * 4);
     A(B.vote, N * 4);

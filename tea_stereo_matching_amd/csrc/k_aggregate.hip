@@ -219,18 +219,18 @@ __global__ __launch_bounds__(AG_THREADS) void k_agg_line(float* __restrict__ vol
 
 void launch_arms(const uint32_t* img, uint32_t* arms, const DevParams& P, hipStream_t st) {
     dim3 g((P.W + 127) / 128, P.H, 2);
-    hipLaunchKernelGGL(k_arms, g, dim3(128), 0, st, img, arms, P);
+    hipLaunchKernelGGL(k_arms, g, dim3(128), 0, st, img, arms, P); trace_point("k_arms", st);
 }
 
 void launch_window_sizes(const uint32_t* arms, int32_t* ws, const DevParams& P, hipStream_t st) {
     dim3 g((P.W + 127) / 128, P.H, 2);
-    hipLaunchKernelGGL(k_window_sizes, g, dim3(128), 0, st, arms, ws, P);
+    hipLaunchKernelGGL(k_window_sizes, g, dim3(128), 0, st, arms, ws, P); trace_point("k_window_sizes", st);
 }
 
 void launch_color_grad(const uint32_t* img, uint8_t* gv, uint8_t* gh, const DevParams& P,
                        hipStream_t st) {
     dim3 g((P.W + 255) / 256, P.H, 2);
-    hipLaunchKernelGGL(k_color_grad, g, dim3(256), 0, st, img, gv, gh, P);
+    hipLaunchKernelGGL(k_color_grad, g, dim3(256), 0, st, img, gv, gh, P); trace_point("k_color_grad", st);
 }
 
 size_t agg_lds_bytes(const DevParams& P) {
@@ -254,10 +254,10 @@ int launch_agg_line(float* vol, const uint32_t* arms, const int32_t* ws, int hor
         attr_set = true;
     }
     switch (J) {
-        case 1: hipLaunchKernelGGL((k_agg_line<1>), g, dim3(AG_THREADS), lds, st, vol, arms, ws, horizontal, A, P); return 0;
-        case 2: hipLaunchKernelGGL((k_agg_line<2>), g, dim3(AG_THREADS), lds, st, vol, arms, ws, horizontal, A, P); return 0;
-        case 3: hipLaunchKernelGGL((k_agg_line<3>), g, dim3(AG_THREADS), lds, st, vol, arms, ws, horizontal, A, P); return 0;
-        case 4: hipLaunchKernelGGL((k_agg_line<4>), g, dim3(AG_THREADS), lds, st, vol, arms, ws, horizontal, A, P); return 0;
+        case 1: hipLaunchKernelGGL((k_agg_line<1>), g, dim3(AG_THREADS), lds, st, vol, arms, ws, horizontal, A, P); trace_point("k_agg_line<1>", st); return 0;
+        case 2: hipLaunchKernelGGL((k_agg_line<2>), g, dim3(AG_THREADS), lds, st, vol, arms, ws, horizontal, A, P); trace_point("k_agg_line<2>", st); return 0;
+        case 3: hipLaunchKernelGGL((k_agg_line<3>), g, dim3(AG_THREADS), lds, st, vol, arms, ws, horizontal, A, P); trace_point("k_agg_line<3>", st); return 0;
+        case 4: hipLaunchKernelGGL((k_agg_line<4>), g, dim3(AG_THREADS), lds, st, vol, arms, ws, horizontal, A, P); trace_point("k_agg_line<4>", st); return 0;
         default: return -1;
     }
 }

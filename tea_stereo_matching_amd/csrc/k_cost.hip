@@ -306,18 +306,18 @@ __global__ __launch_bounds__(CT_THREADS) void k_cost_volume(
 void launch_pack(const uint8_t* left, const uint8_t* right, size_t step, int H, int W,
                  uint32_t* img, hipStream_t st) {
     dim3 g((W + 255) / 256, H, 2);
-    hipLaunchKernelGGL(k_pack_bgr, g, dim3(256), 0, st, left, right, step, H, W, img);
+    hipLaunchKernelGGL(k_pack_bgr, g, dim3(256), 0, st, left, right, step, H, W, img); trace_point("k_pack_bgr", st);
 }
 
 void launch_hsi(const uint32_t* src, uint32_t* tmp, uint32_t* dst, int H, int W, int filter,
                 hipStream_t st) {
     const int n = 2 * H * W;
     if (filter) {
-        hipLaunchKernelGGL(k_bgr2hsi, dim3((n + 255) / 256), dim3(256), 0, st, src, dst, n, 1);
+        hipLaunchKernelGGL(k_bgr2hsi, dim3((n + 255) / 256), dim3(256), 0, st, src, dst, n, 1); trace_point("k_bgr2hsi", st);
     } else {
-        hipLaunchKernelGGL(k_bgr2hsi, dim3((n + 255) / 256), dim3(256), 0, st, src, tmp, n, 0);
+        hipLaunchKernelGGL(k_bgr2hsi, dim3((n + 255) / 256), dim3(256), 0, st, src, tmp, n, 0); trace_point("k_bgr2hsi", st);
         dim3 g((W + 255) / 256, H, 2);
-        hipLaunchKernelGGL(k_gauss_median, g, dim3(256), 0, st, tmp, dst, H, W);
+        hipLaunchKernelGGL(k_gauss_median, g, dim3(256), 0, st, tmp, dst, H, W); trace_point("k_gauss_median", st);
     }
 }
 
@@ -331,6 +331,7 @@ void launch_census(const uint32_t* img, uint32_t* desc, const DevParams& P, hipS
         if (hsi) hipLaunchKernelGGL((k_census_desc<9, 7, true>), g, dim3(128), 0, st, img, desc, P);
         else hipLaunchKernelGGL((k_census_desc<9, 7, false>), g, dim3(128), 0, st, img, desc, P);
     }
+    trace_point("k_census_desc", st);
 }
 
 size_t cost_volume_lds_bytes(const DevParams& P, int lutA_n) {
@@ -344,7 +345,7 @@ static void launch_cost_t(const uint32_t* img, const uint32_t* desc, const float
     dim3 g((P.W + CT - 1) / CT, P.H, 2);
     const size_t lds = cost_volume_lds_bytes(P, lutA_n);
     hipLaunchKernelGGL((k_cost_volume<E, HSI>), g, dim3(CT_THREADS), lds, st, img, desc, lutA,
-                       lutA_n, lutB, vol, P);
+                       lutA_n, lutB, vol, P); trace_point("k_cost_volume<E", st);
 }
 
 int launch_cost_volume(const uint32_t* img, const uint32_t* desc, const float* lutA, int lutA_n,

@@ -583,7 +583,7 @@ size_t refine_scan_blocks(int n) { return (size_t)(n + SC_BLOCK - 1) / SC_BLOCK;
 static dim3 grid2d(int W, int H, int bx) { return dim3((W + bx - 1) / bx, H); }
 
 void launch_outlier(const RefineBufs& B, const DevParams& P, hipStream_t st) {
-    hipLaunchKernelGGL(k_outlier, grid2d(P.W, P.H, 256), dim3(256), 0, st, B.disp0, B.disp1, B.dm, P);
+    hipLaunchKernelGGL(k_outlier, grid2d(P.W, P.H, 256), dim3(256), 0, st, B.disp0, B.disp1, B.dm, P); trace_point("k_outlier", st);
 }
 
 void launch_region_voting(const RefineBufs& B, const uint32_t* arms0, int hf, const DevParams& P,
@@ -591,22 +591,22 @@ void launch_region_voting(const RefineBufs& B, const uint32_t* arms0, int hf, co
     const int n = P.H * P.W;
     const int nb = (int)refine_scan_blocks(n);
     hipLaunchKernelGGL(k_vote_count, grid2d(P.W, P.H, 128), dim3(128), 0, st, B.dm, arms0, B.vote,
-                       B.samples, B.flags, hf, P);
-    hipLaunchKernelGGL(k_scan_count, dim3(nb), dim3(SC_THREADS), 0, st, B.flags, n, B.bsum);
-    hipLaunchKernelGGL(k_scan_blocks, dim3(1), dim3(SC_THREADS), 0, st, B.bsum, nb, B.counts);
+                       B.samples, B.flags, hf, P); trace_point("k_vote_count", st);
+    hipLaunchKernelGGL(k_scan_count, dim3(nb), dim3(SC_THREADS), 0, st, B.flags, n, B.bsum); trace_point("k_scan_count", st);
+    hipLaunchKernelGGL(k_scan_blocks, dim3(1), dim3(SC_THREADS), 0, st, B.bsum, nb, B.counts); trace_point("k_scan_blocks", st);
     hipLaunchKernelGGL(k_scan_scatter, dim3(nb), dim3(SC_THREADS), 0, st, B.flags, n, B.bsum,
-                       B.out_pos, B.out_list, B.hi_list);
+                       B.out_pos, B.out_list, B.hi_list); trace_point("k_scan_scatter", st);
     hipMemcpyAsync(B.dtmp, B.dm, (size_t)n * sizeof(int32_t), hipMemcpyDeviceToDevice, st);
     const size_t lds = (size_t)(VD_THREADS / 64) * P.L * sizeof(int);
     hipLaunchKernelGGL(k_vote_decide, dim3(1024), dim3(VD_THREADS), lds, st, B.dm, B.dtmp, arms0,
-                       B.vote, B.samples, B.out_pos, B.out_list, B.hi_list, B.counts, hf, P);
+                       B.vote, B.samples, B.out_pos, B.out_list, B.hi_list, B.counts, hf, P); trace_point("k_vote_decide", st);
     hipMemcpyAsync(B.dm, B.dtmp, (size_t)n * sizeof(int32_t), hipMemcpyDeviceToDevice, st);
 }
 
 void launch_interpolation(const RefineBufs& B, const uint32_t* img0, const DevParams& P,
                           hipStream_t st) {
     const size_t n = (size_t)P.H * P.W;
-    hipLaunchKernelGGL(k_interp, grid2d(P.W, P.H, 128), dim3(128), 0, st, B.dm, B.dtmp, img0, P);
+    hipLaunchKernelGGL(k_interp, grid2d(P.W, P.H, 128), dim3(128), 0, st, B.dm, B.dtmp, img0, P); trace_point("k_interp", st);
     hipMemcpyAsync(B.dm, B.dtmp, n * sizeof(int32_t), hipMemcpyDeviceToDevice, st);
 }
 
@@ -614,37 +614,37 @@ void launch_discontinuity(const RefineBufs& B, const float* vol0, const DevParam
                           hipStream_t st) {
     const int n = P.H * P.W;
     hipMemsetAsync(B.hist, 0, 256 * sizeof(int32_t), st);
-    hipLaunchKernelGGL(k_gray_hist, dim3(min((n + 255) / 256, 1024)), dim3(256), 0, st, B.dm, B.gray, B.hist, n);
+    hipLaunchKernelGGL(k_gray_hist, dim3(min((n + 255) / 256, 1024)), dim3(256), 0, st, B.dm, B.gray, B.hist, n); trace_point("k_gray_hist", st);
     uint8_t* lut = reinterpret_cast<uint8_t*>(B.hist + 256);
-    hipLaunchKernelGGL(k_eq_lut, dim3(1), dim3(64), 0, st, B.hist, lut, n);
+    hipLaunchKernelGGL(k_eq_lut, dim3(1), dim3(64), 0, st, B.hist, lut, n); trace_point("k_eq_lut", st);
     hipLaunchKernelGGL(k_eq_blur, grid2d(P.W, P.H, 256), dim3(256), 0, st, B.gray, lut,
-                       B.gray_eq, B.blurred, P.H, P.W);
-    hipLaunchKernelGGL(k_sobel, grid2d(P.W, P.H, 256), dim3(256), 0, st, B.blurred, B.dx, B.dy, B.mag, P.H, P.W);
+                       B.gray_eq, B.blurred, P.H, P.W); trace_point("k_eq_blur", st);
+    hipLaunchKernelGGL(k_sobel, grid2d(P.W, P.H, 256), dim3(256), 0, st, B.blurred, B.dx, B.dy, B.mag, P.H, P.W); trace_point("k_sobel", st);
     hipLaunchKernelGGL(k_nms, grid2d(P.W, P.H, 256), dim3(256), 0, st, B.dx, B.dy, B.mag, B.map,
-                       P.H, P.W, P.canny_low, P.canny_high);
-    hipLaunchKernelGGL(k_uf_init, dim3((n + 255) / 256), dim3(256), 0, st, B.map, B.label, n);
-    hipLaunchKernelGGL(k_uf_merge, grid2d(P.W, P.H, 256), dim3(256), 0, st, B.map, B.label, P.H, P.W);
+                       P.H, P.W, P.canny_low, P.canny_high); trace_point("k_nms", st);
+    hipLaunchKernelGGL(k_uf_init, dim3((n + 255) / 256), dim3(256), 0, st, B.map, B.label, n); trace_point("k_uf_init", st);
+    hipLaunchKernelGGL(k_uf_merge, grid2d(P.W, P.H, 256), dim3(256), 0, st, B.map, B.label, P.H, P.W); trace_point("k_uf_merge", st);
     hipMemsetAsync(B.strong, 0, (size_t)n, st);
-    hipLaunchKernelGGL(k_uf_flatten_mark, dim3((n + 255) / 256), dim3(256), 0, st, B.map, B.label, B.strong, n);
-    hipLaunchKernelGGL(k_uf_final, dim3((n + 255) / 256), dim3(256), 0, st, B.map, B.label, B.strong, B.edges, n);
-    hipLaunchKernelGGL(k_adjust, grid2d(P.W, P.H, 256), dim3(256), 0, st, B.dm, B.dtmp, B.edges, vol0, P);
+    hipLaunchKernelGGL(k_uf_flatten_mark, dim3((n + 255) / 256), dim3(256), 0, st, B.map, B.label, B.strong, n); trace_point("k_uf_flatten_mark", st);
+    hipLaunchKernelGGL(k_uf_final, dim3((n + 255) / 256), dim3(256), 0, st, B.map, B.label, B.strong, B.edges, n); trace_point("k_uf_final", st);
+    hipLaunchKernelGGL(k_adjust, grid2d(P.W, P.H, 256), dim3(256), 0, st, B.dm, B.dtmp, B.edges, vol0, P); trace_point("k_adjust", st);
     hipMemcpyAsync(B.dm, B.dtmp, (size_t)n * sizeof(int32_t), hipMemcpyDeviceToDevice, st);
 }
 
 void launch_subpixel_median(const RefineBufs& B, const float* vol0, const uint32_t* orig_left,
                             float* out, size_t out_step, int roi_or_mask, int offset,
                             const DevParams& P, hipStream_t st) {
-    hipLaunchKernelGGL(k_subpix, grid2d(P.W, P.H, 256), dim3(256), 0, st, B.dm, vol0, B.subpix, P);
+    hipLaunchKernelGGL(k_subpix, grid2d(P.W, P.H, 256), dim3(256), 0, st, B.dm, vol0, B.subpix, P); trace_point("k_subpix", st);
     hipLaunchKernelGGL(k_median_out, grid2d(P.W, P.H, 256), dim3(256), 0, st, B.subpix, out,
-                       out_step, orig_left, roi_or_mask, offset, P.H, P.W);
+                       out_step, orig_left, roi_or_mask, offset, P.H, P.W); trace_point("k_median_out", st);
 }
 
 void launch_vol_to_ref(const float* vol, float* ref, int views, const DevParams& P, hipStream_t st) {
-    hipLaunchKernelGGL(k_vol_to_ref, dim3(256, P.L, views), dim3(256), 0, st, vol, ref, P);
+    hipLaunchKernelGGL(k_vol_to_ref, dim3(256, P.L, views), dim3(256), 0, st, vol, ref, P); trace_point("k_vol_to_ref", st);
 }
 
 void launch_arms_to_ref(const uint32_t* arms, int32_t* ref, const DevParams& P, hipStream_t st) {
-    hipLaunchKernelGGL(k_arms_to_ref, dim3(256, 2), dim3(256), 0, st, arms, ref, P);
+    hipLaunchKernelGGL(k_arms_to_ref, dim3(256, 2), dim3(256), 0, st, arms, ref, P); trace_point("k_arms_to_ref", st);
 }
 
 }  // namespace tsm

@@ -303,10 +303,10 @@ int launch_scan_vertical(float* vol, const uint8_t* gv, const uint32_t* img, int
     const int J = (P.Lp / 4 + 63) / 64;
     dim3 g((P.W + 3) / 4, 2);
     switch (J) {
-        case 1: hipLaunchKernelGGL((k_scan_vertical<1>), g, dim3(256), 0, st, vol, gv, img, dir, P); return 0;
-        case 2: hipLaunchKernelGGL((k_scan_vertical<2>), g, dim3(256), 0, st, vol, gv, img, dir, P); return 0;
-        case 3: hipLaunchKernelGGL((k_scan_vertical<3>), g, dim3(256), 0, st, vol, gv, img, dir, P); return 0;
-        case 4: hipLaunchKernelGGL((k_scan_vertical<4>), g, dim3(256), 0, st, vol, gv, img, dir, P); return 0;
+        case 1: hipLaunchKernelGGL((k_scan_vertical<1>), g, dim3(256), 0, st, vol, gv, img, dir, P); trace_point("k_scan_vertical<1>", st); return 0;
+        case 2: hipLaunchKernelGGL((k_scan_vertical<2>), g, dim3(256), 0, st, vol, gv, img, dir, P); trace_point("k_scan_vertical<2>", st); return 0;
+        case 3: hipLaunchKernelGGL((k_scan_vertical<3>), g, dim3(256), 0, st, vol, gv, img, dir, P); trace_point("k_scan_vertical<3>", st); return 0;
+        case 4: hipLaunchKernelGGL((k_scan_vertical<4>), g, dim3(256), 0, st, vol, gv, img, dir, P); trace_point("k_scan_vertical<4>", st); return 0;
         default: return -1;
     }
 }
@@ -316,10 +316,10 @@ int launch_scan_horizontal(float* vol, const uint8_t* gh, const uint32_t* img, i
     const int J = (P.Lp / 4 + 63) / 64;
     dim3 g((P.H + 3) / 4, 2);
     switch (J) {
-        case 1: hipLaunchKernelGGL((k_scan_horizontal<1>), g, dim3(256), 0, st, vol, gh, img, dir, wta, store_view1, P); return 0;
-        case 2: hipLaunchKernelGGL((k_scan_horizontal<2>), g, dim3(256), 0, st, vol, gh, img, dir, wta, store_view1, P); return 0;
-        case 3: hipLaunchKernelGGL((k_scan_horizontal<3>), g, dim3(256), 0, st, vol, gh, img, dir, wta, store_view1, P); return 0;
-        case 4: hipLaunchKernelGGL((k_scan_horizontal<4>), g, dim3(256), 0, st, vol, gh, img, dir, wta, store_view1, P); return 0;
+        case 1: hipLaunchKernelGGL((k_scan_horizontal<1>), g, dim3(256), 0, st, vol, gh, img, dir, wta, store_view1, P); trace_point("k_scan_horizontal<1>", st); return 0;
+        case 2: hipLaunchKernelGGL((k_scan_horizontal<2>), g, dim3(256), 0, st, vol, gh, img, dir, wta, store_view1, P); trace_point("k_scan_horizontal<2>", st); return 0;
+        case 3: hipLaunchKernelGGL((k_scan_horizontal<3>), g, dim3(256), 0, st, vol, gh, img, dir, wta, store_view1, P); trace_point("k_scan_horizontal<3>", st); return 0;
+        case 4: hipLaunchKernelGGL((k_scan_horizontal<4>), g, dim3(256), 0, st, vol, gh, img, dir, wta, store_view1, P); trace_point("k_scan_horizontal<4>", st); return 0;
         default: return -1;
     }
 }

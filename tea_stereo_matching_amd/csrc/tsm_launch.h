@@ -8,6 +8,10 @@
 
 namespace tsm {
 
+// Debug hook (engine.cpp): with TSM_TRACE=1 in the environment, synchronise the stream
+// after every launch and log the kernel name + status to stderr.  No-op otherwise.
+void trace_point(const char* what, hipStream_t st);
+
 // k_cost.hip
 void launch_pack(const uint8_t* left, const uint8_t* right, size_t step, int H, int W,
                  uint32_t* img, hipStream_t st);

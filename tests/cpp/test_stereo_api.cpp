@@ -1,0 +1,69 @@
+// C++ API check (run by tests/test_gpu_cpp_api.py on the GPU box): the reference's
+// usage pattern (README.md:177-191) against stereo::ADCensus from include/stereo.h,
+// including the reference's exception types and messages.
+#include <cstdio>
+#include <cstdlib>
+#include <string>
+#include <vector>
+
+#include "stereo.h"
+
+static int fails = 0;
+#define CHECK(c)                                                    \
+    do {                                                            \
+        if (!(c)) { std::printf("FAIL %s:%d %s\n", __FILE__, __LINE__, #c); ++fails; } \
+    } while (0)
+
+template <typename F>
+static std::string thrown_string(F f) {
+    try { f(); } catch (const std::string& s) { return s; } catch (...) { return "<other>"; }
+    return "<none>";
+}
+
+int main() {
+    const int H = 48, W = 80;
+    std::vector<unsigned char> l(H * W * 3), r(H * W * 3);
+    unsigned s = 12345;
+    for (int y = 0; y < H; ++y)
+        for (int x = 0; x < W; ++x)
+            for (int c = 0; c < 3; ++c) {
+                s = s * 1664525u + 1013904223u;
+                l[(y * W + x) * 3 + c] = (unsigned char)(64 + ((x / 4 + y / 4 + c) * 37 + (s >> 28)) % 128);
+            }
+    for (int y = 0; y < H; ++y)  // right view = left shifted by 6 px
+        for (int x = 0; x < W; ++x)
+            for (int c = 0; c < 3; ++c) r[(y * W + x) * 3 + c] = l[(y * W + std::min(W - 1, x + 6)) * 3 + c];
+
+    stereo::ADCensus adcensus;
+    adcensus.setMatchingStrategy(stereo::ColorModel::RGB, false, false);
+    adcensus.setMinMaxDisparity(0, 16);
+    stereo::ImageView L{l.data(), H, W, (size_t)W * 3}, R{r.data(), H, W, (size_t)W * 3};
+    stereo::DisparityMap d;
+    adcensus.compute(L, R, d);
+    CHECK(d.rows == H && d.cols == W && (int)d.data.size() == H * W);
+    int six = 0, valid = 0;
+    for (float v : d.data) { if (v >= 0) { ++valid; if (v > 5.5f && v < 6.5f) ++six; } }
+    CHECK(valid > H * W / 2);
+    CHECK(six > valid * 8 / 10);
+
+    CHECK(thrown_string([&] { adcensus.setMinMaxDisparity(-3, 3); }) == "[ADCensus] Set MinMaxDisparity error.");
+    CHECK(thrown_string([&] { adcensus.setMinMaxDisparity(9, 9); }) == "[ADCensus] Set MinMaxDisparity error.");
+    CHECK(thrown_string([&] { adcensus.setOffset(-1); }) == "[ADCensus] Offset must be positive.");
+    stereo::ImageView bad{l.data(), H, W - 1, (size_t)W * 3};
+    CHECK(thrown_string([&] { adcensus.compute(L, bad, d); }) == "[ADCensus] Image error.");
+    stereo::ImageView empty{};
+    CHECK(thrown_string([&] { adcensus.compute(empty, R, d); }) == "[ADCensus] Image error.");
+
+    std::vector<stereo::ImageView> ls{L, L}, rs{R, R};
+    std::vector<stereo::DisparityMap> ds;
+    adcensus.compute(ls, rs, ds);
+    CHECK(ds.size() == 2 && ds[0].data == d.data && ds[1].data == d.data);
+
+    // StereoMatching polymorphism, as the reference's callers use it
+    stereo::StereoMatching* sm = &adcensus;
+    stereo::DisparityMap d2;
+    sm->compute(L, R, d2);
+    CHECK(d2.data == d.data);
+    std::printf("%s (%d failures)\n", fails ? "FAILED" : "OK", fails);
+    return fails ? 1 : 0;
+}

@@ -193,3 +193,54 @@ def test_default_state_is_reference_default(tsm):
     p = m.params()
     assert (p.color_thresh1, p.max_length1, p.color_diff) == (5, 17, 3)  # HSI set (:413-414)
     m.close()
+
+
+def test_hsi_mode_against_oracle(matcher, tsm, oracle):
+    """HSI ("Selective AD-Census-HSI", the reference's default model).  bgr2hsi uses
+    acosf (device libm vs glibc): the converted images may differ in rare hue bytes, so
+    the images are compared with a tolerance and the disparity on >= 99 % of pixels."""
+    left, right = _synthetic(tsm, 31, 72, 120, 33)
+    d_g, g = _gpu(matcher, tsm, left, right, 1, 0, 32, ("images",))
+    d_o, o = oracle.compute(left, right, _oracle_params(oracle, oracle.HSI, 0, 32), ("images",))
+    img_diff = np.abs(g["images"].astype(int) - o["images"].astype(int))
+    assert (img_diff <= 1).all()
+    assert (img_diff > 0).mean() < 1e-3
+    if (img_diff == 0).all():
+        assert np.array_equal(d_g, d_o)
+    valid = d_o >= 0
+    assert (np.abs(d_g - d_o)[valid] <= 0.5).mean() >= 0.99
+
+
+@pytest.mark.parametrize("roi,mask", [(True, False), (False, True)])
+def test_roi_mask_modes(matcher, tsm, oracle, roi, mask):
+    """ROI / mask matching: maxD := W/2 (:339-340), black pixels excluded from costs,
+    arms and scanline (:459-460, :551-555, :625-629, :824, :862), offset and background
+    rules on the output (:388-403, :1415-1427)."""
+    left, right = _synthetic(tsm, 41, 64, 100, 51)
+    left[:, :12] = 0    # black (masked) band
+    right[:, -9:] = 0
+    matcher.setOffset(3)
+    d_g, _ = _gpu(matcher, tsm, left, right, 0, 0, 50, roi=roi, mask=mask)
+    matcher.setOffset(0)
+    p = _oracle_params(oracle, oracle.RGB, 0, 50, roi_matching=int(roi), mask_matching=int(mask),
+                       offset=3)
+    d_o, _ = oracle.compute(left, right, p)
+    assert np.array_equal(d_g, d_o)
+    assert matcher.getMinMaxDisparity() == (0, 50)  # maxD = W/2 persists (:340)
+
+
+def test_census_7x5_window(matcher, tsm, oracle):
+    """CensusWin::CENSUSWIN_7x5 (stereo_utils.h:203) through tsm_adc_set_params."""
+    left, right = _synthetic(tsm, 51, 64, 96, 25)
+    matcher.setMatchingStrategy(tsm.ColorModel.RGB)
+    p = matcher.params()
+    p.census_win = 1
+    matcher.setParams(p)
+    matcher.setMinMaxDisparity(0, 24)
+    matcher.setOmpEmulation(0)
+    d_g, g = matcher.compute_debug(left, right, STAGES)
+    d_o, o = oracle.compute(left, right, _oracle_params(oracle, oracle.RGB, 0, 24, census_win=1), STAGES)
+    _assert_stages_equal(g, o, STAGES)
+    assert np.array_equal(d_g, d_o)
+    matcher.setMatchingStrategy(tsm.ColorModel.RGB)  # resets the parameter set
+    assert matcher.params().census_win == 0

@@ -18,6 +18,7 @@ step() {  # step <name> <timeout-s> <cmd...>
 for s in "$@"; do
     case $s in
         smoke) step smoke 300 python3 -c "import __graft_entry__ as g; g.smoke()" ;;
+        trace) export TSM_TRACE=1; step trace 120 python3 -u -c "import __graft_entry__ as g; g.smoke()"; unset TSM_TRACE ;;
         tests) step gpu_tests 900 python3 -m pytest tests -x -q -m gpu ;;
         tests-k) step gpu_tests 900 python3 -m pytest tests -q -m gpu ;;
         bench) step bench 600 python3 bench.py ;;
