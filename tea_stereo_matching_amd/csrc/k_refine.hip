@@ -14,12 +14,21 @@
 //                                    (OpenCV 4.x semantics) -> edge-pixel adjustment;
 //                                    Canny hysteresis as lock-free union-find
 //   subpixelEnhancement :1344-1374   parabola fit + medianBlur 3x3 (fp32, replicate)
+#include <utility>
+
 #include "tsm_device.h"
 #include "tsm_launch.h"
 
 namespace tsm {
 
 constexpr int kMaxSamples = 20; // = votingThresh: a low-vote outlier holds <= 20 samples
+
+// zero-fill on the stream by a kernel (keeps every producer/consumer inside the
+// kernel-ordering domain; no DMA-engine writes between kernels)
+__global__ void k_zero_u32(uint32_t* __restrict__ p, int n) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) p[i] = 0u;
+}
 
 // ---------------------------------------------------------------------------
 // outlier elimination (LR check)
@@ -53,7 +62,8 @@ __device__ __forceinline__ void region_arms(uint32_t a, bool hf, int& oA, int& o
 
 // Per pixel: vote count of outliers (+ up to 20 samples for low-vote ones) and flags
 // (bit0 outlier, bit1 high-vote).
-__global__ void k_vote_count(const int32_t* __restrict__ disp, const uint32_t* __restrict__ arms,
+__global__ void k_vote_count(const int32_t* __restrict__ disp, int32_t* __restrict__ dtmp,
+                             const uint32_t* __restrict__ arms,
                              int32_t* __restrict__ vote, uint16_t* __restrict__ samples,
                              uint8_t* __restrict__ flags, int hf, DevParams P) {
     const int x = blockIdx.x * blockDim.x + threadIdx.x;
@@ -62,6 +72,7 @@ __global__ void k_vote_count(const int32_t* __restrict__ disp, const uint32_t* _
     if (x >= W) return;
     const size_t idx = (size_t)y * W + x;
     const int minD = P.minD;
+    dtmp[idx] = disp[idx]; // dispTemp starts as the input; k_vote_decide overwrites high-vote outliers
     if (disp[idx] >= minD) { flags[idx] = 0; vote[idx] = 0; return; }
     int oA, oB, iA, iB;
     region_arms(arms[idx], hf, oA, oB, iA, iB);
@@ -582,38 +593,37 @@ size_t refine_scan_blocks(int n) { return (size_t)(n + SC_BLOCK - 1) / SC_BLOCK;
 
 static dim3 grid2d(int W, int H, int bx) { return dim3((W + bx - 1) / bx, H); }
 
-void launch_outlier(const RefineBufs& B, const DevParams& P, hipStream_t st) {
+void launch_outlier(RefineBufs& B, const DevParams& P, hipStream_t st) {
     hipLaunchKernelGGL(k_outlier, grid2d(P.W, P.H, 256), dim3(256), 0, st, B.disp0, B.disp1, B.dm, P); trace_point("k_outlier", st);
 }
 
-void launch_region_voting(const RefineBufs& B, const uint32_t* arms0, int hf, const DevParams& P,
+// Each Jacobi stage reads B.dm, writes B.dtmp, then the two maps swap roles (no copies).
+void launch_region_voting(RefineBufs& B, const uint32_t* arms0, int hf, const DevParams& P,
                           hipStream_t st) {
     const int n = P.H * P.W;
     const int nb = (int)refine_scan_blocks(n);
-    hipLaunchKernelGGL(k_vote_count, grid2d(P.W, P.H, 128), dim3(128), 0, st, B.dm, arms0, B.vote,
-                       B.samples, B.flags, hf, P); trace_point("k_vote_count", st);
+    hipLaunchKernelGGL(k_vote_count, grid2d(P.W, P.H, 128), dim3(128), 0, st, B.dm, B.dtmp, arms0,
+                       B.vote, B.samples, B.flags, hf, P); trace_point("k_vote_count", st);
     hipLaunchKernelGGL(k_scan_count, dim3(nb), dim3(SC_THREADS), 0, st, B.flags, n, B.bsum); trace_point("k_scan_count", st);
     hipLaunchKernelGGL(k_scan_blocks, dim3(1), dim3(SC_THREADS), 0, st, B.bsum, nb, B.counts); trace_point("k_scan_blocks", st);
     hipLaunchKernelGGL(k_scan_scatter, dim3(nb), dim3(SC_THREADS), 0, st, B.flags, n, B.bsum,
                        B.out_pos, B.out_list, B.hi_list); trace_point("k_scan_scatter", st);
-    hipMemcpyAsync(B.dtmp, B.dm, (size_t)n * sizeof(int32_t), hipMemcpyDeviceToDevice, st);
     const size_t lds = (size_t)(VD_THREADS / 64) * P.L * sizeof(int);
     hipLaunchKernelGGL(k_vote_decide, dim3(1024), dim3(VD_THREADS), lds, st, B.dm, B.dtmp, arms0,
                        B.vote, B.samples, B.out_pos, B.out_list, B.hi_list, B.counts, hf, P); trace_point("k_vote_decide", st);
-    hipMemcpyAsync(B.dm, B.dtmp, (size_t)n * sizeof(int32_t), hipMemcpyDeviceToDevice, st);
+    std::swap(B.dm, B.dtmp);
 }
 
-void launch_interpolation(const RefineBufs& B, const uint32_t* img0, const DevParams& P,
+void launch_interpolation(RefineBufs& B, const uint32_t* img0, const DevParams& P,
                           hipStream_t st) {
-    const size_t n = (size_t)P.H * P.W;
     hipLaunchKernelGGL(k_interp, grid2d(P.W, P.H, 128), dim3(128), 0, st, B.dm, B.dtmp, img0, P); trace_point("k_interp", st);
-    hipMemcpyAsync(B.dm, B.dtmp, n * sizeof(int32_t), hipMemcpyDeviceToDevice, st);
+    std::swap(B.dm, B.dtmp);
 }
 
-void launch_discontinuity(const RefineBufs& B, const float* vol0, const DevParams& P,
+void launch_discontinuity(RefineBufs& B, const float* vol0, const DevParams& P,
                           hipStream_t st) {
     const int n = P.H * P.W;
-    hipMemsetAsync(B.hist, 0, 256 * sizeof(int32_t), st);
+    hipLaunchKernelGGL(k_zero_u32, dim3(1), dim3(256), 0, st, reinterpret_cast<uint32_t*>(B.hist), 256); trace_point("k_zero_u32", st);
     hipLaunchKernelGGL(k_gray_hist, dim3(min((n + 255) / 256, 1024)), dim3(256), 0, st, B.dm, B.gray, B.hist, n); trace_point("k_gray_hist", st);
     uint8_t* lut = reinterpret_cast<uint8_t*>(B.hist + 256);
     hipLaunchKernelGGL(k_eq_lut, dim3(1), dim3(64), 0, st, B.hist, lut, n); trace_point("k_eq_lut", st);
@@ -624,11 +634,11 @@ void launch_discontinuity(const RefineBufs& B, const float* vol0, const DevParam
                        P.H, P.W, P.canny_low, P.canny_high); trace_point("k_nms", st);
     hipLaunchKernelGGL(k_uf_init, dim3((n + 255) / 256), dim3(256), 0, st, B.map, B.label, n); trace_point("k_uf_init", st);
     hipLaunchKernelGGL(k_uf_merge, grid2d(P.W, P.H, 256), dim3(256), 0, st, B.map, B.label, P.H, P.W); trace_point("k_uf_merge", st);
-    hipMemsetAsync(B.strong, 0, (size_t)n, st);
+    hipLaunchKernelGGL(k_zero_u32, dim3((n / 4 + 256) / 256), dim3(256), 0, st, reinterpret_cast<uint32_t*>(B.strong), (n + 3) / 4); trace_point("k_zero_u32", st);
     hipLaunchKernelGGL(k_uf_flatten_mark, dim3((n + 255) / 256), dim3(256), 0, st, B.map, B.label, B.strong, n); trace_point("k_uf_flatten_mark", st);
     hipLaunchKernelGGL(k_uf_final, dim3((n + 255) / 256), dim3(256), 0, st, B.map, B.label, B.strong, B.edges, n); trace_point("k_uf_final", st);
     hipLaunchKernelGGL(k_adjust, grid2d(P.W, P.H, 256), dim3(256), 0, st, B.dm, B.dtmp, B.edges, vol0, P); trace_point("k_adjust", st);
-    hipMemcpyAsync(B.dm, B.dtmp, (size_t)n * sizeof(int32_t), hipMemcpyDeviceToDevice, st);
+    std::swap(B.dm, B.dtmp);
 }
 
 void launch_subpixel_median(const RefineBufs& B, const float* vol0, const uint32_t* orig_left,

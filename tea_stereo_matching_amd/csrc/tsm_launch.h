@@ -65,12 +65,12 @@ struct RefineBufs {
     float* subpix;    // [H][W]
 };
 size_t refine_scan_blocks(int n);
-void launch_outlier(const RefineBufs& B, const DevParams& P, hipStream_t st);
-void launch_region_voting(const RefineBufs& B, const uint32_t* arms0, int horizontal_first,
+void launch_outlier(RefineBufs& B, const DevParams& P, hipStream_t st);
+void launch_region_voting(RefineBufs& B, const uint32_t* arms0, int horizontal_first,
                           const DevParams& P, hipStream_t st);
-void launch_interpolation(const RefineBufs& B, const uint32_t* img0, const DevParams& P,
+void launch_interpolation(RefineBufs& B, const uint32_t* img0, const DevParams& P,
                           hipStream_t st);
-void launch_discontinuity(const RefineBufs& B, const float* vol0, const DevParams& P,
+void launch_discontinuity(RefineBufs& B, const float* vol0, const DevParams& P,
                           hipStream_t st);
 void launch_subpixel_median(const RefineBufs& B, const float* vol0, const uint32_t* orig_left,
                             float* out, size_t out_step, int roi_or_mask, int offset,
