@@ -241,6 +241,13 @@ __global__ __launch_bounds__(VD_THREADS) void k_vote_decide(
 // ---------------------------------------------------------------------------
 // proper interpolation
 // ---------------------------------------------------------------------------
+// 16 rays of (:1166-1167); the reference steps d/2 then d - d/2 (C++ truncating /2).
+__constant__ int c_ray_h[16] = {2, 2, 0, -2, -2, -2, 0, 2, 2, 1, -1, -2, -2, -1, 1, 2};
+__constant__ int c_ray_w[16] = {0, 2, 2, 2, 0, -2, -2, -2, 1, 2, 2, 1, -1, -2, -2, -1};
+
+// The per-ray results are folded as each ray finishes, in ray order, which is exactly
+// the reference's two post-loops (:1211-1216 min for occlusions, :1222-1231 colour-diff
+// selection for mismatches): no per-thread arrays, no dynamic register indexing.
 __global__ void k_interp(const int32_t* __restrict__ disp, int32_t* __restrict__ out,
                          const uint32_t* __restrict__ img0, DevParams P) {
     const int x = blockIdx.x * blockDim.x + threadIdx.x;
@@ -250,39 +257,35 @@ __global__ void k_interp(const int32_t* __restrict__ disp, int32_t* __restrict__
     const size_t idx = (size_t)y * W + x;
     const int cur = disp[idx];
     if (cur >= minD) { out[idx] = cur; return; }
-    const int dWt[16] = {0, 2, 2, 2, 0, -2, -2, -2, 1, 2, 2, 1, -1, -2, -2, -1};
-    const int dHt[16] = {2, 2, 0, -2, -2, -2, 0, 2, 2, 1, -1, -2, -2, -1, 1, 2};
-    int nd[16], ndiff[16];
+    const bool occlusion = cur == minD - 1; // :1209
     const uint32_t c0 = img0[idx];
+    int res = cur;        // occlusion: running min;  mismatch: md
+    int mdiff = -1;       // mismatch: running mdiff
     for (int dir = 0; dir < 16; ++dir) {
-        nd[dir] = cur;
-        ndiff[dir] = -1;
+        const int sh0 = c_ray_h[dir] / 2, sh1 = c_ray_h[dir] - c_ray_h[dir] / 2;
+        const int sw0 = c_ray_w[dir] / 2, sw1 = c_ray_w[dir] - c_ray_w[dir] / 2;
+        int nd = cur, ndiff = -1;
         int hD = y, wD = x;
-        bool inside = true, got = false;
-        for (int s = 0; s < P.max_search_depth && inside && !got; ++s) {
-            if (s % 2 == 0) { hD += dHt[dir] / 2; wD += dWt[dir] / 2; }
-            else { hD += dHt[dir] - dHt[dir] / 2; wD += dWt[dir] - dWt[dir] / 2; }
-            inside = hD >= 0 && hD < H && wD >= 0 && wD < W;
-            if (inside) {
-                const int dv = disp[(size_t)hD * W + wD];
-                if (dv >= minD) {
-                    nd[dir] = dv;
-                    ndiff[dir] = color_diff(P, c0, img0[(size_t)hD * W + wD]);
-                    got = true;
-                }
+        for (int s = 0; s < P.max_search_depth; ++s) {
+            hD += (s & 1) ? sh1 : sh0;
+            wD += (s & 1) ? sw1 : sw0;
+            if (hD < 0 || hD >= H || wD < 0 || wD >= W) break;
+            const int dv = disp[(size_t)hD * W + wD];
+            if (dv >= minD) {
+                nd = dv;
+                ndiff = color_diff(P, c0, img0[(size_t)hD * W + wD]);
+                break;
             }
         }
-    }
-    int res;
-    if (cur == minD - 1) { // occlusion (:1209)
-        res = nd[0];
-        for (int k = 1; k < 16; ++k) res = min(res, nd[k]);
-    } else {
-        int md = nd[0], mdiff = ndiff[0];
-        for (int k = 1; k < 16; ++k) {
-            if (mdiff < 0 || (mdiff > ndiff[k] && ndiff[k] > 0)) { md = nd[k]; mdiff = ndiff[k]; }
+        if (occlusion) {
+            res = dir == 0 ? nd : min(res, nd);
+        } else if (dir == 0) {
+            res = nd;
+            mdiff = ndiff;
+        } else if (mdiff < 0 || (mdiff > ndiff && ndiff > 0)) {
+            res = nd;
+            mdiff = ndiff;
         }
-        res = md;
     }
     out[idx] = res;
 }
