@@ -23,6 +23,10 @@ for s in "$@"; do
         tests-k) step gpu_tests 900 python3 -m pytest tests -q -m gpu ;;
         bench) step bench 600 python3 bench.py ;;
         bench-short) step bench 400 python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline ;;
+        prof) cd /tmp && export TMPDIR=/tmp && cd "$OLDPWD"
+              step prof 600 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof -o run -- python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline ;;
+        pmc-fetch) step pmc_fetch 600 rocprofv3 --pmc FETCH_SIZE --output-format csv -d gpurun_out/pmc_fetch -o run -- python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline --batch 2 ;;
+        pmc-write) step pmc_write 600 rocprofv3 --pmc WRITE_SIZE --output-format csv -d gpurun_out/pmc_write -o run -- python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline --batch 2 ;;
         *) echo "unknown step $s"; exit 2 ;;
     esac
 done
