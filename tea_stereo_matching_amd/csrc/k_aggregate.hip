@@ -122,20 +122,43 @@ __global__ void k_color_grad(const uint32_t* __restrict__ img, uint8_t* __restri
 }
 
 // ---------------------------------------------------------------------------
-// 1-D aggregation along lines, in place, LDS ring
+// 1-D aggregation along lines, in place, LDS ring with register-staged prefetch
 // ---------------------------------------------------------------------------
-constexpr int AG_SEG = 16;     // outputs per step (4 per wave)
-constexpr int AG_THREADS = 256;
+// One 512-thread workgroup owns a whole line of one view.  Per step it produces SEG
+// outputs (4 per wave) from the LDS ring, while the SEG pixel vectors of the NEXT step
+// are already in flight into registers (issued before the compute, written to the ring
+// after the barrier), so HBM latency hides behind the compute.  The line's packed arms
+// and window sizes are staged in LDS once, so the per-output arm lookup is an LDS
+// broadcast instead of a dependent global load.
+constexpr int AG_SEG = 32;
+constexpr int AG_THREADS = 512;
+constexpr int AG_WAVES = AG_THREADS / 64;
+constexpr int AG_PER_WAVE = AG_SEG / AG_WAVES;  // outputs per wave per step
 
-// copy pixels [x0, x1) of the line into their ring slots (flattened float4 index t = px*Q + q:
-// consecutive threads read consecutive 16-B pieces of a pixel's L-vector)
-__device__ __forceinline__ void agg_fill(float4* ring, int RING, const float* base, size_t es, int Q,
-                                         int x0, int x1, int tid) {
+template <int PF>
+__device__ __forceinline__ void agg_issue(f32x4 (&pf)[PF], const float* __restrict__ base, size_t es,
+                                          int Q, int x0, int x1, int tid) {
     const int cnt = (x1 - x0) * Q;
-    for (int t = tid; t < cnt; t += AG_THREADS) {
-        const int px = t / Q, q = t - px * Q;
-        ring[((x0 + px) % RING) * Q + q] =
-            *reinterpret_cast<const float4*>(base + (size_t)(x0 + px) * es + 4 * q);
+#pragma unroll
+    for (int r = 0; r < PF; ++r) {
+        const int t = tid + r * AG_THREADS;
+        const int tt = t < cnt ? t : 0;  // clamp: keeps every slot's load unconditional
+        const int px = tt / Q, q = tt - px * Q;
+        pf[r] = *reinterpret_cast<const f32x4*>(base + (size_t)(x0 + px) * es + 4 * q);
+    }
+}
+
+template <int PF>
+__device__ __forceinline__ void agg_commit(const f32x4 (&pf)[PF], f32x4* ring, int RING, int Q,
+                                           int x0, int x1, int tid) {
+    const int cnt = (x1 - x0) * Q;
+#pragma unroll
+    for (int r = 0; r < PF; ++r) {
+        const int t = tid + r * AG_THREADS;
+        if (t < cnt) {
+            const int px = t / Q, q = t - px * Q;
+            ring[((x0 + px) % RING) * Q + q] = pf[r];
+        }
     }
 }
 
@@ -144,7 +167,8 @@ __global__ __launch_bounds__(AG_THREADS) void k_agg_line(float* __restrict__ vol
                                                          const uint32_t* __restrict__ arms,
                                                          const int32_t* __restrict__ ws,
                                                          int horizontal, int A, DevParams P) {
-    extern __shared__ __attribute__((aligned(16))) float4 ring[];
+    constexpr int PF = (AG_SEG * 64 * J + AG_THREADS - 1) / AG_THREADS;  // float4 per thread per step
+    extern __shared__ __attribute__((aligned(16))) f32x4 smem_f4[];
     const int H = P.H, W = P.W, Lp = P.Lp;
     const int Q = Lp >> 2;                      // float4 per pixel vector
     const int RING = AG_SEG + 2 * A;
@@ -157,62 +181,70 @@ __global__ __launch_bounds__(AG_THREADS) void k_agg_line(float* __restrict__ vol
     const size_t as = horizontal ? 1 : (size_t)W;
     const int32_t* wsl = ws ? ws + (size_t)v * 2 * H * W + (horizontal ? (size_t)line * W : (size_t)line) : nullptr;
     const int shA = horizontal ? 16 : 0, shB = horizontal ? 24 : 8;
+    f32x4* ring = smem_f4;
+    uint32_t* arm_s = reinterpret_cast<uint32_t*>(ring + (size_t)RING * Q);
+    float* ws_s = reinterpret_cast<float*>(arm_s + n);
 
     const int tid = threadIdx.x;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int lane = tid & 63;
     const int nsteps = (n + AG_SEG - 1) / AG_SEG;
 
-    // initial window [0, min(n, SEG + A))
-    agg_fill(ring, RING, base, es, Q, 0, min(n, AG_SEG + A), tid);
+    f32x4 pf[PF];
+    agg_issue<PF>(pf, base, es, Q, 0, min(n, AG_SEG), tid);
+    for (int i = tid; i < n; i += AG_THREADS) {
+        const uint32_t a = ab[(size_t)i * as];
+        arm_s[i] = (((a >> shA) & 0xffu) << 16) | ((a >> shB) & 0xffu);  // lo<<16 | hi
+        if (wsl) ws_s[i] = (float)wsl[(size_t)i * as];
+    }
+    agg_commit<PF>(pf, ring, RING, Q, 0, min(n, AG_SEG), tid);
+    // rest of the initial window [SEG, SEG + A)
+    for (int x0 = AG_SEG; x0 < min(n, AG_SEG + A); x0 += AG_SEG) {
+        const int x1 = min(min(n, AG_SEG + A), x0 + AG_SEG);
+        agg_issue<PF>(pf, base, es, Q, x0, x1, tid);
+        agg_commit<PF>(pf, ring, RING, Q, x0, x1, tid);
+    }
     __syncthreads();
 
     for (int s = 0; s < nsteps; ++s) {
-        // the pixels step s+1 adds: [(s+1)*SEG + A, (s+2)*SEG + A)
+        // the pixels step s+1 adds: [(s+1)*SEG + A, (s+2)*SEG + A), loads in flight now
         const int nx0 = min(n, (s + 1) * AG_SEG + A);
         const int nx1 = min(n, (s + 2) * AG_SEG + A);
+        if (nx0 < nx1) agg_issue<PF>(pf, base, es, Q, nx0, nx1, tid);
 
-        for (int i = 0; i < AG_SEG / 4; ++i) {
-            const int o = s * AG_SEG + wave * (AG_SEG / 4) + i;
-            if (o >= n) break;
-            const uint32_t a = ab[(size_t)o * as];
-            const int lo = (a >> shA) & 0xff, hi = (a >> shB) & 0xff;
-            float4 acc[J];
 #pragma unroll
-            for (int j = 0; j < J; ++j) acc[j] = make_float4(0.f, 0.f, 0.f, 0.f);
-            int slot = (o - lo) % RING;
-            for (int k = -lo; k <= hi; ++k) {
+        for (int i = 0; i < AG_PER_WAVE; ++i) {
+            const int o = s * AG_SEG + wave * AG_PER_WAVE + i;
+            if (o < n) {
+                const uint32_t a = arm_s[o];
+                const int lo = (int)(a >> 16), hi = (int)(a & 0xffffu);
+                f32x4 acc[J];
+#pragma unroll
+                for (int j = 0; j < J; ++j) acc[j] = f32x4{0.f, 0.f, 0.f, 0.f};
+                int slot = o - lo;
+                slot = slot >= RING ? slot % RING : slot;
+                for (int k = -lo; k <= hi; ++k) {
+#pragma unroll
+                    for (int j = 0; j < J; ++j) {
+                        const int q = lane + 64 * j;
+                        if (q < Q) acc[j] += ring[slot * Q + q];  // 4 independent sequential fp32 sums
+                    }
+                    slot = slot + 1 == RING ? 0 : slot + 1;
+                }
+                if (wsl) {
+                    const float wsz = ws_s[o];
+#pragma unroll
+                    for (int j = 0; j < J; ++j) acc[j] /= wsz;
+                }
 #pragma unroll
                 for (int j = 0; j < J; ++j) {
                     const int q = lane + 64 * j;
-                    if (q < Q) {
-                        const float4 x = ring[slot * Q + q];
-                        acc[j].x += x.x;
-                        acc[j].y += x.y;
-                        acc[j].z += x.z;
-                        acc[j].w += x.w;
-                    }
+                    if (q < Q) *reinterpret_cast<f32x4*>(base + (size_t)o * es + 4 * q) = acc[j];
                 }
-                slot = slot + 1 == RING ? 0 : slot + 1;
-            }
-            if (wsl) {
-                const float wsz = (float)wsl[(size_t)o * as];
-#pragma unroll
-                for (int j = 0; j < J; ++j) {
-                    acc[j].x /= wsz;
-                    acc[j].y /= wsz;
-                    acc[j].z /= wsz;
-                    acc[j].w /= wsz;
-                }
-            }
-#pragma unroll
-            for (int j = 0; j < J; ++j) {
-                const int q = lane + 64 * j;
-                if (q < Q) *reinterpret_cast<float4*>(base + (size_t)o * es + 4 * q) = acc[j];
             }
         }
         __syncthreads(); // everyone done reading the slots about to be overwritten
-        if (nx0 < nx1) agg_fill(ring, RING, base, es, Q, nx0, nx1, tid);
+        if (nx0 < nx1) agg_commit<PF>(pf, ring, RING, Q, nx0, nx1, tid);
         __syncthreads();
     }
 }
@@ -235,7 +267,8 @@ void launch_color_grad(const uint32_t* img, uint8_t* gv, uint8_t* gh, const DevP
 
 size_t agg_lds_bytes(const DevParams& P) {
     const int A = P.max_length1 - 1;
-    return (size_t)(AG_SEG + 2 * A) * (P.Lp / 4) * sizeof(float4);
+    const int nmax = P.W > P.H ? P.W : P.H;
+    return (size_t)(AG_SEG + 2 * A) * (P.Lp / 4) * 16 + (size_t)nmax * 8;
 }
 
 int launch_agg_line(float* vol, const uint32_t* arms, const int32_t* ws, int horizontal,
@@ -249,17 +282,15 @@ int launch_agg_line(float* vol, const uint32_t* arms, const int32_t* ws, int hor
     if (!attr_set) {
         hipFuncSetAttribute((const void*)k_agg_line<1>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
         hipFuncSetAttribute((const void*)k_agg_line<2>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-        hipFuncSetAttribute((const void*)k_agg_line<3>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-        hipFuncSetAttribute((const void*)k_agg_line<4>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
         attr_set = true;
     }
     switch (J) {
-        case 1: hipLaunchKernelGGL((k_agg_line<1>), g, dim3(AG_THREADS), lds, st, vol, arms, ws, horizontal, A, P); trace_point("k_agg_line<1>", st); return 0;
-        case 2: hipLaunchKernelGGL((k_agg_line<2>), g, dim3(AG_THREADS), lds, st, vol, arms, ws, horizontal, A, P); trace_point("k_agg_line<2>", st); return 0;
-        case 3: hipLaunchKernelGGL((k_agg_line<3>), g, dim3(AG_THREADS), lds, st, vol, arms, ws, horizontal, A, P); trace_point("k_agg_line<3>", st); return 0;
-        case 4: hipLaunchKernelGGL((k_agg_line<4>), g, dim3(AG_THREADS), lds, st, vol, arms, ws, horizontal, A, P); trace_point("k_agg_line<4>", st); return 0;
+        case 1: hipLaunchKernelGGL((k_agg_line<1>), g, dim3(AG_THREADS), lds, st, vol, arms, ws, horizontal, A, P); break;
+        case 2: hipLaunchKernelGGL((k_agg_line<2>), g, dim3(AG_THREADS), lds, st, vol, arms, ws, horizontal, A, P); break;
         default: return -1;
     }
+    trace_point("k_agg_line", st);
+    return 0;
 }
 
 }  // namespace tsm

@@ -35,81 +35,83 @@ __device__ __forceinline__ bool omp_chunk_start(int it, int n, int T) {
 }
 
 template <int J>
-__device__ __forceinline__ float vec_min(const float4 (&x)[J], int lane, int Q, int L) {
+__device__ __forceinline__ float vec_min(const f32x4 (&x)[J], int lane, int Q, int L, int from = 0) {
     float m = __int_as_float(0x7f800000);
 #pragma unroll
     for (int j = 0; j < J; ++j) {
         const int q = lane + 64 * j;
         if (q < Q) {
             const int d = 4 * q;
-            if (d + 0 < L) m = fminf(m, x[j].x);
-            if (d + 1 < L) m = fminf(m, x[j].y);
-            if (d + 2 < L) m = fminf(m, x[j].z);
-            if (d + 3 < L) m = fminf(m, x[j].w);
+#pragma unroll
+            for (int e = 0; e < 4; ++e)
+                if (d + e < L && d + e >= from) m = fminf(m, x[j][e]);
         }
     }
     return wave_min_nonneg(m);
 }
 
-// WTA over indices [minD, L-1] with the first minimum winning (strict <, :1404).
+// WTA over indices [minD, L-1], first minimum (strict <, ADCensus.cpp:1404): the first d
+// whose cost equals the wave minimum, found by a ballot (no 64-bit shuffle reduction).
+// `m` is the wave min over [0, L); recomputed over [minD, L) when minD > 0.
 template <int J>
-__device__ __forceinline__ int vec_argmin(const float4 (&x)[J], int lane, int Q, int L, int minD) {
-    uint64_t best = ~0ull;
+__device__ __forceinline__ int vec_argmin(const f32x4 (&x)[J], int lane, int Q, int L, int minD, float m) {
+    if (minD > 0) m = vec_min<J>(x, lane, Q, L, minD);
+    if (!(m < 3.402823466e+38f)) return minD;  // nothing below FLT_MAX: reference leaves it unset
 #pragma unroll
     for (int j = 0; j < J; ++j) {
         const int q = lane + 64 * j;
+        int first = 4;
         if (q < Q) {
-            const float e[4] = {x[j].x, x[j].y, x[j].z, x[j].w};
 #pragma unroll
-            for (int k = 0; k < 4; ++k) {
-                const int d = 4 * q + k;
-                if (d >= minD && d < L) {
-                    const uint64_t key = ((uint64_t)__float_as_uint(e[k]) << 32) | (uint32_t)d;
-                    best = key < best ? key : best;
-                }
+            for (int e = 3; e >= 0; --e) {
+                const int d = 4 * q + e;
+                if (d < L && d >= minD && x[j][e] == m) first = e;
             }
         }
+        const uint64_t mask = __ballot(first < 4);
+        if (mask) {
+            const int ln = __builtin_ctzll(mask);
+            const int e = __builtin_amdgcn_readlane(first, ln);
+            return 4 * (ln + 64 * j) + e;
+        }
     }
-    best = wave_min_u64(best);
-    const uint32_t bits = (uint32_t)(best >> 32);
-    // nothing strictly below FLT_MAX: the reference leaves the pixel uninitialised; we
-    // return minD (defined behaviour, same as the oracle).
-    if (best == ~0ull || !(__uint_as_float(bits) < 3.402823466e+38f)) return minD;
-    return (int)(uint32_t)best;
+    return minD;
 }
 
-// One partialOptimization step for the wave's pixel p given predecessor q (registers).
-//   gsel(d) returns d2 (colour difference on the other view at the shifted column).
-template <int J, typename G>
-__device__ __forceinline__ void partial_opt(float4 (&p)[J], const float4 (&q)[J], float mq, int d1,
-                                            G gsel, int lane, int Q, const DevParams& P) {
+// One partialOptimization step (ADCensus.cpp:869-913) for the wave's pixel p given its
+// predecessor q (registers).  g[j] packs the four d2 bytes (other-view colour difference,
+// or colorDiff+1 when out of range) of this lane's disparities.
+template <int J>
+__device__ __forceinline__ void partial_opt(f32x4 (&p)[J], const f32x4 (&q)[J], float mq, int d1,
+                                            const uint32_t (&g)[J], int lane, int Q, const DevParams& P) {
     const int L = P.L;
     const int cd = P.color_diff;
     const int s1 = d1 < cd ? 1 : 0;
 #pragma unroll
     for (int j = 0; j < J; ++j) {
         // neighbours across the float4 boundary: d-1 of element 0, d+1 of element 3
-        float lo = dpp_f<DPP_WAVE_SHR1>(q[j].w, 0.f);
-        float hi = dpp_f<DPP_WAVE_SHL1>(q[j].x, 0.f);
+        float lo = dpp_f<DPP_WAVE_SHR1>(q[j][3], 0.f);
+        float hi = dpp_f<DPP_WAVE_SHL1>(q[j][0], 0.f);
         if (j > 0) {
-            const float prev = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(q[j - 1].w), 63));
+            const float prev = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(q[j - 1][3]), 63));
             if (lane == 0) lo = prev;
         }
         if (j + 1 < J) {
-            const float nxt = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(q[j + 1].x), 0));
+            const float nxt = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(q[j + 1][0]), 0));
             if (lane == 63) hi = nxt;
         }
         const int qi = lane + 64 * j;
         if (qi >= Q) continue;
-        const float qe[6] = {lo, q[j].x, q[j].y, q[j].z, q[j].w, hi};
-        float pe[4] = {p[j].x, p[j].y, p[j].z, p[j].w};
+        const float qe[6] = {lo, q[j][0], q[j][1], q[j][2], q[j][3], hi};
+        f32x4 pe = p[j];
 #pragma unroll
         for (int k = 0; k < 4; ++k) {
             const int d = 4 * qi + k;
             if (d >= L) break;
-            const int d2 = gsel(d);
+            const int d2 = (g[j] >> (8 * k)) & 0xff;
             const int cnt = s1 + (d2 < cd ? 1 : 0);
-            const float p1 = P.p1t[cnt], p2 = P.p2t[cnt];
+            const float p1 = cnt == 2 ? P.p1t[2] : (cnt == 1 ? P.p1t[1] : P.p1t[0]);
+            const float p2 = cnt == 2 ? P.p2t[2] : (cnt == 1 ? P.p2t[1] : P.p2t[0]);
             const float cost = pe[k] - mq;
             float mo = mq + p2;
             const float t0 = qe[k + 1];
@@ -124,204 +126,193 @@ __device__ __forceinline__ void partial_opt(float4 (&p)[J], const float4 (&q)[J]
             }
             pe[k] = (cost + mo) / 2;
         }
-        p[j] = make_float4(pe[0], pe[1], pe[2], pe[3]);
-    }
-}
-
-template <int J>
-__device__ __forceinline__ void load_vec(float4 (&x)[J], const float* ptr, int lane, int Q) {
-#pragma unroll
-    for (int j = 0; j < J; ++j) {
-        const int q = lane + 64 * j;
-        if (q < Q) x[j] = *reinterpret_cast<const float4*>(ptr + 4 * q);
-        else x[j] = make_float4(0.f, 0.f, 0.f, 0.f);
-    }
-}
-template <int J>
-__device__ __forceinline__ void store_vec(const float4 (&x)[J], float* ptr, int lane, int Q) {
-#pragma unroll
-    for (int j = 0; j < J; ++j) {
-        const int q = lane + 64 * j;
-        if (q < Q) *reinterpret_cast<float4*>(ptr + 4 * q) = x[j];
+        p[j] = pe;
     }
 }
 
 // ---------------------------------------------------------------------------
-// vertical passes: one wave per (column, view); dir = +1 (down) or -1 (up)
+// One wave walks one line (a column for vertical passes, a row for horizontal ones) of
+// one view.  Everything a step needs that does not depend on the chain -- the pixel's
+// L-vector, the uniform d1 and the per-disparity d2 bytes -- is prefetched K steps ahead
+// into a register ring, so the serial critical path is only the update + wave min.
+// The leftward horizontal pass is the last one: it emits the WTA disparity of every
+// pixel and, for view 1 (only needed for the WTA), can skip storing the volume.
 // ---------------------------------------------------------------------------
-template <int J>
-__global__ __launch_bounds__(256) void k_scan_vertical(float* __restrict__ vol,
-                                                       const uint8_t* __restrict__ gv,
-                                                       const uint32_t* __restrict__ img,
-                                                       int dir, DevParams P) {
+constexpr int SC_K = 8;  // prefetch depth (steps)
+
+template <int J, bool HORIZ>
+struct LineStep {
+    f32x4 p[J];
+    uint32_t g[J];
+    int d1;
+};
+
+template <int J, bool HORIZ>
+__device__ __forceinline__ void scan_issue(LineStep<J, HORIZ>& st, int it, int n, int dir, int line,
+                                           const float* base, size_t es, const uint8_t* gown,
+                                           const uint8_t* goth, int sgn, int lane, int Q,
+                                           const DevParams& P) {
+    const int len = n + 1;
+    const int pos = dir > 0 ? 1 + it : len - 2 - it;  // w1 (HORIZ) or h1 (vertical)
+    const int pm = dir > 0 ? pos : pos + 1;            // max(pos, predecessor)
+    const float* ptr = base + (size_t)pos * es;
+#pragma unroll
+    for (int j = 0; j < J; ++j) {
+        const int q = lane + 64 * j;
+        st.p[j] = q < Q ? *reinterpret_cast<const f32x4*>(ptr + 4 * q) : f32x4{0.f, 0.f, 0.f, 0.f};
+    }
+    const int W = P.W;
+    const int cd1 = P.color_diff + 1;
+    if (HORIZ) {
+        st.d1 = gown[pm];
+        const int off = dir > 0 ? 0 : 1;  // max(x1, x2) - x1
+#pragma unroll
+        for (int j = 0; j < J; ++j) {
+            uint32_t g = 0;
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+                const int d = 4 * (lane + 64 * j) + e;
+                const int x1 = pos + sgn * (d + P.minD);
+                const int x2 = x1 - dir;
+                const bool in = x1 >= 0 && x1 < W && x2 >= 0 && x2 < W && d < P.L;
+                const uint32_t b = in ? goth[x1 + off] : (uint32_t)cd1;
+                g |= b << (8 * e);
+            }
+            st.g[j] = g;
+        }
+    } else {
+        st.d1 = gown[(size_t)pm * W + line];
+        const uint8_t* grow = goth + (size_t)pm * W;
+#pragma unroll
+        for (int j = 0; j < J; ++j) {
+            uint32_t g = 0;
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+                const int d = 4 * (lane + 64 * j) + e;
+                const int x = line + sgn * (d + P.minD);
+                const uint32_t b = (x >= 0 && x < W && d < P.L) ? grow[x] : (uint32_t)cd1;
+                g |= b << (8 * e);
+            }
+            st.g[j] = g;
+        }
+    }
+}
+
+template <int J, bool HORIZ>
+__global__ __launch_bounds__(256) void k_scan_line(float* __restrict__ vol,
+                                                   const uint8_t* __restrict__ grad,
+                                                   const uint32_t* __restrict__ img, int dir,
+                                                   int32_t* __restrict__ wta, int store_view1,
+                                                   DevParams P) {
     const int H = P.H, W = P.W, Lp = P.Lp, Q = Lp >> 2;
     const int lane = threadIdx.x & 63;
-    const int w = __builtin_amdgcn_readfirstlane(blockIdx.x * 4 + (threadIdx.x >> 6));
+    const int line = __builtin_amdgcn_readfirstlane(blockIdx.x * 4 + (threadIdx.x >> 6));
     const int v = blockIdx.y;
-    if (w >= W) return;
-    const size_t rs = (size_t)W * Lp; // floats per image row
-    float* col = vol + (size_t)v * H * rs + (size_t)w * Lp;
-    const uint8_t* gown = gv + (size_t)v * H * W;
-    const uint8_t* goth = gv + (size_t)(1 - v) * H * W;
+    if (line >= (HORIZ ? H : W)) return;
+    const int len = HORIZ ? W : H;
+    const size_t es = HORIZ ? (size_t)Lp : (size_t)W * Lp;
+    float* base = vol + (size_t)v * H * W * Lp + (HORIZ ? (size_t)line * W * Lp : (size_t)line * Lp);
+    const uint8_t* gown = grad + (size_t)v * H * W + (HORIZ ? (size_t)line * W : 0);
+    const uint8_t* goth = grad + (size_t)(1 - v) * H * W + (HORIZ ? (size_t)line * W : 0);
     const uint32_t* im = img + (size_t)v * H * W;
     const int sgn = v == 0 ? 1 : -1;
-    const int n = H - 1;
+    const int n = len - 1;
     const int T = P.omp_threads;
+    const bool store = !(wta && v == 1 && !store_view1);
+    int32_t* wrow = wta ? wta + ((size_t)v * H + line) * W : nullptr;  // only HORIZ passes emit WTA
 
-    float4 q[J], p[J], pn[J];
-    const int h0 = dir > 0 ? 0 : H - 1;
-    load_vec<J>(q, col + (size_t)h0 * rs, lane, Q);
+    f32x4 q[J];
+    const int p0 = dir > 0 ? 0 : len - 1;
+#pragma unroll
+    for (int j = 0; j < J; ++j) {
+        const int qq = lane + 64 * j;
+        q[j] = qq < Q ? *reinterpret_cast<const f32x4*>(base + (size_t)p0 * es + 4 * qq) : f32x4{0.f, 0.f, 0.f, 0.f};
+    }
     float mq = vec_min<J>(q, lane, Q, P.L);
-    float4 qorig[J];
+    if (wrow) {
+        const int d = vec_argmin<J>(q, lane, Q, P.L, P.minD, mq);
+        if (lane == 0) wrow[p0] = d;
+    }
+    f32x4 qorig[J];
     float mqorig = mq;
 #pragma unroll
     for (int j = 0; j < J; ++j) qorig[j] = q[j];
-    if (n > 0) load_vec<J>(pn, col + (size_t)(dir > 0 ? 1 : H - 2) * rs, lane, Q);
-    for (int it = 0; it < n; ++it) {
-        const int h1 = dir > 0 ? 1 + it : H - 2 - it;
-        const int h2 = h1 - dir;
+
+    LineStep<J, HORIZ> ring[SC_K];
 #pragma unroll
-        for (int j = 0; j < J; ++j) p[j] = pn[j];
-        if (it + 1 < n) load_vec<J>(pn, col + (size_t)(h1 + dir) * rs, lane, Q);
-        if (T > 1 && omp_chunk_start(it, n, T)) { // stale predecessor (racy schedule)
+    for (int k = 0; k < SC_K; ++k)
+        if (k < n) scan_issue<J, HORIZ>(ring[k], k, n, dir, line, base, es, gown, goth, sgn, lane, Q, P);
+
+    for (int b = 0; b < n; b += SC_K) {
 #pragma unroll
-            for (int j = 0; j < J; ++j) q[j] = qorig[j];
-            mq = mqorig;
+        for (int k = 0; k < SC_K; ++k) {
+            const int it = b + k;
+            if (it < n) {
+                f32x4 p[J];
+                uint32_t g[J];
+#pragma unroll
+                for (int j = 0; j < J; ++j) { p[j] = ring[k].p[j]; g[j] = ring[k].g[j]; }
+                const int d1 = ring[k].d1;
+                if (it + SC_K < n)
+                    scan_issue<J, HORIZ>(ring[k], it + SC_K, n, dir, line, base, es, gown, goth, sgn, lane, Q, P);
+                const int pos = dir > 0 ? 1 + it : len - 2 - it;
+                const int pred = pos - dir;
+                if (T > 1 && omp_chunk_start(it, n, T)) {  // stale predecessor (racy schedule)
+#pragma unroll
+                    for (int j = 0; j < J; ++j) q[j] = qorig[j];
+                    mq = mqorig;
+                }
+                const bool keep = T > 1 && omp_chunk_start(it + 1, n, T);
+                if (keep) {
+#pragma unroll
+                    for (int j = 0; j < J; ++j) qorig[j] = p[j];
+                    mqorig = vec_min<J>(p, lane, Q, P.L);
+                }
+                const bool masked = P.mask && (HORIZ ? im[(size_t)line * W + pred] : im[(size_t)pred * W + line]) == 0;
+                if (!(masked || mq == 0.f)) {  // :880-881 -- else p stays untouched
+                    partial_opt<J>(p, q, mq, d1, g, lane, Q, P);
+                    if (store) {
+#pragma unroll
+                        for (int j = 0; j < J; ++j) {
+                            const int qq = lane + 64 * j;
+                            if (qq < Q) *reinterpret_cast<f32x4*>(base + (size_t)pos * es + 4 * qq) = p[j];
+                        }
+                    }
+                }
+#pragma unroll
+                for (int j = 0; j < J; ++j) q[j] = p[j];
+                mq = vec_min<J>(q, lane, Q, P.L);
+                if (wrow) {
+                    const int d = vec_argmin<J>(q, lane, Q, P.L, P.minD, mq);
+                    if (lane == 0) wrow[pos] = d;
+                }
+            }
         }
-        // keep this pixel's pre-pass vector for a possible chunk start at it+1
-        const bool keep = T > 1 && omp_chunk_start(it + 1, n, T);
-        if (keep) {
-#pragma unroll
-            for (int j = 0; j < J; ++j) qorig[j] = p[j];
-            mqorig = vec_min<J>(p, lane, Q, P.L);
-        }
-        const bool masked = P.mask && im[(size_t)h2 * W + w] == 0; // :824
-        if (masked || mq == 0.f) { // :880-881 -- p untouched
-#pragma unroll
-            for (int j = 0; j < J; ++j) q[j] = p[j];
-            mq = keep ? mqorig : vec_min<J>(p, lane, Q, P.L);
-            continue;
-        }
-        const int hm = h1 > h2 ? h1 : h2;
-        const int d1 = gown[(size_t)hm * W + w];
-        const uint8_t* grow = goth + (size_t)hm * W;
-        const int minD = P.minD, cd1 = P.color_diff + 1;
-        auto gsel = [&](int d) -> int {
-            const int x = w + sgn * (d + minD);
-            return (x >= 0 && x < W) ? (int)grow[x] : cd1;
-        };
-        partial_opt<J>(p, q, mq, d1, gsel, lane, Q, P);
-        store_vec<J>(p, col + (size_t)h1 * rs, lane, Q);
-#pragma unroll
-        for (int j = 0; j < J; ++j) q[j] = p[j];
-        mq = vec_min<J>(q, lane, Q, P.L);
     }
 }
 
-// ---------------------------------------------------------------------------
-// horizontal passes: one wave per (row, view); dir = +1 (rightward) or -1 (leftward).
-// The leftward pass is the last one: it emits the WTA disparity of every pixel and,
-// for view 1 (only needed for the WTA), can skip storing the volume.
-// ---------------------------------------------------------------------------
-template <int J>
-__global__ __launch_bounds__(256) void k_scan_horizontal(float* __restrict__ vol,
-                                                         const uint8_t* __restrict__ gh,
-                                                         const uint32_t* __restrict__ img,
-                                                         int dir, int32_t* __restrict__ wta,
-                                                         int store_view1, DevParams P) {
-    const int H = P.H, W = P.W, Lp = P.Lp, Q = Lp >> 2;
-    const int lane = threadIdx.x & 63;
-    const int h = __builtin_amdgcn_readfirstlane(blockIdx.x * 4 + (threadIdx.x >> 6));
-    const int v = blockIdx.y;
-    if (h >= H) return;
-    float* row = vol + ((size_t)v * H + h) * W * Lp;
-    const uint8_t* gown = gh + ((size_t)v * H + h) * W;
-    const uint8_t* goth = gh + ((size_t)(1 - v) * H + h) * W;
-    const uint32_t* im = img + ((size_t)v * H + h) * W;
-    const int sgn = v == 0 ? 1 : -1;
-    const int n = W - 1;
-    const int T = P.omp_threads;
-    const bool store = !(wta && v == 1 && !store_view1);
-    int32_t* wrow = wta ? wta + ((size_t)v * H + h) * W : nullptr;
-
-    float4 q[J], p[J], pn[J];
-    const int w0 = dir > 0 ? 0 : W - 1;
-    load_vec<J>(q, row + (size_t)w0 * Lp, lane, Q);
-    float mq = vec_min<J>(q, lane, Q, P.L);
-    if (wrow) {
-        const int d = vec_argmin<J>(q, lane, Q, P.L, P.minD);
-        if (lane == 0) wrow[w0] = d;
+template <bool HORIZ>
+static int launch_scan(float* vol, const uint8_t* grad, const uint32_t* img, int dir, int32_t* wta,
+                       int store_view1, const DevParams& P, hipStream_t st) {
+    const int J = (P.Lp / 4 + 63) / 64;
+    dim3 g(((HORIZ ? P.H : P.W) + 3) / 4, 2);
+    switch (J) {
+        case 1: hipLaunchKernelGGL((k_scan_line<1, HORIZ>), g, dim3(256), 0, st, vol, grad, img, dir, wta, store_view1, P); break;
+        case 2: hipLaunchKernelGGL((k_scan_line<2, HORIZ>), g, dim3(256), 0, st, vol, grad, img, dir, wta, store_view1, P); break;
+        default: return -1;
     }
-    float4 qorig[J];
-    float mqorig = mq;
-#pragma unroll
-    for (int j = 0; j < J; ++j) qorig[j] = q[j];
-    if (n > 0) load_vec<J>(pn, row + (size_t)(dir > 0 ? 1 : W - 2) * Lp, lane, Q);
-    for (int it = 0; it < n; ++it) {
-        const int w1 = dir > 0 ? 1 + it : W - 2 - it;
-        const int w2 = w1 - dir;
-#pragma unroll
-        for (int j = 0; j < J; ++j) p[j] = pn[j];
-        if (it + 1 < n) load_vec<J>(pn, row + (size_t)(w1 + dir) * Lp, lane, Q);
-        if (T > 1 && omp_chunk_start(it, n, T)) {
-#pragma unroll
-            for (int j = 0; j < J; ++j) q[j] = qorig[j];
-            mq = mqorig;
-        }
-        const bool keep = T > 1 && omp_chunk_start(it + 1, n, T);
-        if (keep) {
-#pragma unroll
-            for (int j = 0; j < J; ++j) qorig[j] = p[j];
-            mqorig = vec_min<J>(p, lane, Q, P.L);
-        }
-        const bool masked = P.mask && im[w2] == 0; // :862
-        if (!(masked || mq == 0.f)) {
-            const int d1 = gown[w1 > w2 ? w1 : w2];
-            const int minD = P.minD, cd1 = P.color_diff + 1;
-            const int off = dir > 0 ? 0 : 1; // max(x1, x2) - x1
-            auto gsel = [&](int d) -> int {
-                const int x1 = w1 + sgn * (d + minD);
-                const int x2 = w2 + sgn * (d + minD);
-                const bool in = x1 >= 0 && x1 < W && x2 >= 0 && x2 < W;
-                return in ? (int)goth[x1 + off] : cd1;
-            };
-            partial_opt<J>(p, q, mq, d1, gsel, lane, Q, P);
-            if (store) store_vec<J>(p, row + (size_t)w1 * Lp, lane, Q);
-        }
-#pragma unroll
-        for (int j = 0; j < J; ++j) q[j] = p[j];
-        mq = vec_min<J>(q, lane, Q, P.L);
-        if (wrow) {
-            const int d = vec_argmin<J>(q, lane, Q, P.L, P.minD);
-            if (lane == 0) wrow[w1] = d;
-        }
-    }
+    trace_point(HORIZ ? "k_scan_line<H>" : "k_scan_line<V>", st);
+    return 0;
 }
 
 int launch_scan_vertical(float* vol, const uint8_t* gv, const uint32_t* img, int dir,
                          const DevParams& P, hipStream_t st) {
-    const int J = (P.Lp / 4 + 63) / 64;
-    dim3 g((P.W + 3) / 4, 2);
-    switch (J) {
-        case 1: hipLaunchKernelGGL((k_scan_vertical<1>), g, dim3(256), 0, st, vol, gv, img, dir, P); trace_point("k_scan_vertical<1>", st); return 0;
-        case 2: hipLaunchKernelGGL((k_scan_vertical<2>), g, dim3(256), 0, st, vol, gv, img, dir, P); trace_point("k_scan_vertical<2>", st); return 0;
-        case 3: hipLaunchKernelGGL((k_scan_vertical<3>), g, dim3(256), 0, st, vol, gv, img, dir, P); trace_point("k_scan_vertical<3>", st); return 0;
-        case 4: hipLaunchKernelGGL((k_scan_vertical<4>), g, dim3(256), 0, st, vol, gv, img, dir, P); trace_point("k_scan_vertical<4>", st); return 0;
-        default: return -1;
-    }
+    return launch_scan<false>(vol, gv, img, dir, nullptr, 1, P, st);
 }
 
 int launch_scan_horizontal(float* vol, const uint8_t* gh, const uint32_t* img, int dir,
                            int32_t* wta, int store_view1, const DevParams& P, hipStream_t st) {
-    const int J = (P.Lp / 4 + 63) / 64;
-    dim3 g((P.H + 3) / 4, 2);
-    switch (J) {
-        case 1: hipLaunchKernelGGL((k_scan_horizontal<1>), g, dim3(256), 0, st, vol, gh, img, dir, wta, store_view1, P); trace_point("k_scan_horizontal<1>", st); return 0;
-        case 2: hipLaunchKernelGGL((k_scan_horizontal<2>), g, dim3(256), 0, st, vol, gh, img, dir, wta, store_view1, P); trace_point("k_scan_horizontal<2>", st); return 0;
-        case 3: hipLaunchKernelGGL((k_scan_horizontal<3>), g, dim3(256), 0, st, vol, gh, img, dir, wta, store_view1, P); trace_point("k_scan_horizontal<3>", st); return 0;
-        case 4: hipLaunchKernelGGL((k_scan_horizontal<4>), g, dim3(256), 0, st, vol, gh, img, dir, wta, store_view1, P); trace_point("k_scan_horizontal<4>", st); return 0;
-        default: return -1;
-    }
+    return launch_scan<true>(vol, gh, img, dir, wta, store_view1, P, st);
 }
 
 }  // namespace tsm

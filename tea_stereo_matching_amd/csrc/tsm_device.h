@@ -17,6 +17,11 @@ namespace tsm {
 
 constexpr int kWave = 64;
 
+// native 4-wide vectors: register arrays of these stay in VGPRs (HIP's float4 class
+// type defeats SROA in arrays and spills them to scratch)
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+
 // POD kernel parameters (ADCensusParams, stereo_utils.h:209-244, plus geometry).
 struct DevParams {
     int H, W;          // image size
