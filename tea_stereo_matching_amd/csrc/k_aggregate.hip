@@ -56,7 +56,8 @@ __device__ int compute_limit(const DevParams& P, const uint32_t* __restrict__ im
 }
 
 // arms[v][y][x] = up | down<<8 | left<<16 | right<<24  (computeLimits, :661-683)
-__global__ void k_arms(const uint32_t* __restrict__ img, uint32_t* __restrict__ arms, DevParams P) {
+__global__ void k_arms(const uint32_t* __restrict__ img, uint32_t* __restrict__ arms, DevParams Pk) {
+    const DevParams P = Pk;  // kernel args -> registers once (no per-use kernarg reloads)
     const int x = blockIdx.x * blockDim.x + threadIdx.x;
     const int y = blockIdx.y;
     const int v = blockIdx.z;
@@ -82,7 +83,8 @@ __device__ __forceinline__ int arm_right(uint32_t a) { return (a >> 24) & 0xff; 
 // same way for each slice, :716), so they are computed once per view and orientation.
 //   ws[v][0]: horizontalFirst (row counts then column sums), ws[v][1]: vertical first.
 __global__ void k_window_sizes(const uint32_t* __restrict__ arms, int32_t* __restrict__ ws,
-                               DevParams P) {
+                               DevParams Pk) {
+    const DevParams P = Pk;  // kernel args -> registers once (no per-use kernarg reloads)
     const int x = blockIdx.x * blockDim.x + threadIdx.x;
     const int y = blockIdx.y;
     const int v = blockIdx.z;
@@ -108,7 +110,8 @@ __global__ void k_window_sizes(const uint32_t* __restrict__ arms, int32_t* __res
 //   gv[v][y][x] = colorDiff(img_v(y,x), img_v(y-1,x))  (y >= 1)
 //   gh[v][y][x] = colorDiff(img_v(y,x), img_v(y,x-1))  (x >= 1)
 __global__ void k_color_grad(const uint32_t* __restrict__ img, uint8_t* __restrict__ gv,
-                             uint8_t* __restrict__ gh, DevParams P) {
+                             uint8_t* __restrict__ gh, DevParams Pk) {
+    const DevParams P = Pk;  // kernel args -> registers once (no per-use kernarg reloads)
     const int x = blockIdx.x * blockDim.x + threadIdx.x;
     const int y = blockIdx.y;
     const int v = blockIdx.z;
@@ -166,7 +169,8 @@ template <int J>
 __global__ __launch_bounds__(AG_THREADS) void k_agg_line(float* __restrict__ vol,
                                                          const uint32_t* __restrict__ arms,
                                                          const int32_t* __restrict__ ws,
-                                                         int horizontal, int A, DevParams P) {
+                                                         int horizontal, int A, DevParams Pk) {
+    const DevParams P = Pk;  // kernel args -> registers once (no per-use kernarg reloads)
     constexpr int PF = (AG_SEG * 64 * J + AG_THREADS - 1) / AG_THREADS;  // float4 per thread per step
     extern __shared__ __attribute__((aligned(16))) f32x4 smem_f4[];
     const int H = P.H, W = P.W, Lp = P.Lp;

@@ -109,7 +109,8 @@ __global__ void k_gauss_median(const uint32_t* __restrict__ src, uint32_t* __res
 // ---------------------------------------------------------------------------
 template <int CW, int CHh, bool HSI>
 __global__ void k_census_desc(const uint32_t* __restrict__ img, uint32_t* __restrict__ desc,
-                              DevParams P) {
+                              DevParams Pk) {
+    const DevParams P = Pk;  // kernel args -> registers once (no per-use kernarg reloads)
     const int x = blockIdx.x * blockDim.x + threadIdx.x;
     const int y = blockIdx.y;
     const int v = blockIdx.z;
@@ -175,7 +176,8 @@ template <int E, bool HSI>
 __global__ __launch_bounds__(CT_THREADS) void k_cost_volume(
     const uint32_t* __restrict__ img, const uint32_t* __restrict__ desc,
     const float* __restrict__ lutA, int lutA_n, const float* __restrict__ lutB,
-    float* __restrict__ vol, DevParams P) {
+    float* __restrict__ vol, DevParams Pk) {
+    const DevParams P = Pk;  // kernel args -> registers once (no per-use kernarg reloads)
     extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
     const int H = P.H, W = P.W, L = P.L, Lp = P.Lp;
     const int v = blockIdx.z;

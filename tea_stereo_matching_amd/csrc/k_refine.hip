@@ -34,7 +34,8 @@ __global__ void k_zero_u32(uint32_t* __restrict__ p, int n) {
 // outlier elimination (LR check)
 // ---------------------------------------------------------------------------
 __global__ void k_outlier(const int32_t* __restrict__ dl, const int32_t* __restrict__ dr,
-                          int32_t* __restrict__ out, DevParams P) {
+                          int32_t* __restrict__ out, DevParams Pk) {
+    const DevParams P = Pk;  // kernel args -> registers once (no per-use kernarg reloads)
     const int x = blockIdx.x * blockDim.x + threadIdx.x;
     const int y = blockIdx.y;
     const int W = P.W;
@@ -65,7 +66,8 @@ __device__ __forceinline__ void region_arms(uint32_t a, bool hf, int& oA, int& o
 __global__ void k_vote_count(const int32_t* __restrict__ disp, int32_t* __restrict__ dtmp,
                              const uint32_t* __restrict__ arms,
                              int32_t* __restrict__ vote, uint16_t* __restrict__ samples,
-                             uint8_t* __restrict__ flags, int hf, DevParams P) {
+                             uint8_t* __restrict__ flags, int hf, DevParams Pk) {
+    const DevParams P = Pk;  // kernel args -> registers once (no per-use kernarg reloads)
     const int x = blockIdx.x * blockDim.x + threadIdx.x;
     const int y = blockIdx.y;
     const int W = P.W;
@@ -186,7 +188,8 @@ __global__ __launch_bounds__(VD_THREADS) void k_vote_decide(
     const int32_t* __restrict__ disp, int32_t* __restrict__ dtmp, const uint32_t* __restrict__ arms,
     const int32_t* __restrict__ vote, const uint16_t* __restrict__ samples,
     const int32_t* __restrict__ out_pos, const int32_t* __restrict__ out_list,
-    const int32_t* __restrict__ hi_list, const int32_t* __restrict__ counts, int hf, DevParams P) {
+    const int32_t* __restrict__ hi_list, const int32_t* __restrict__ counts, int hf, DevParams Pk) {
+    const DevParams P = Pk;  // kernel args -> registers once (no per-use kernarg reloads)
     extern __shared__ int hist_all[];
     const int L = P.L, W = P.W, minD = P.minD;
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
@@ -249,7 +252,8 @@ __constant__ int c_ray_w[16] = {0, 2, 2, 2, 0, -2, -2, -2, 1, 2, 2, 1, -1, -2, -
 // the reference's two post-loops (:1211-1216 min for occlusions, :1222-1231 colour-diff
 // selection for mismatches): no per-thread arrays, no dynamic register indexing.
 __global__ void k_interp(const int32_t* __restrict__ disp, int32_t* __restrict__ out,
-                         const uint32_t* __restrict__ img0, DevParams P) {
+                         const uint32_t* __restrict__ img0, DevParams Pk) {
+    const DevParams P = Pk;  // kernel args -> registers once (no per-use kernarg reloads)
     const int x = blockIdx.x * blockDim.x + threadIdx.x;
     const int y = blockIdx.y;
     const int H = P.H, W = P.W, minD = P.minD;
@@ -476,7 +480,8 @@ __global__ void k_uf_final(const uint8_t* __restrict__ map, const int32_t* __res
 // discontinuityAdjustment body (:1266-1339); reads the pre-adjust map, writes dtmp.
 __global__ void k_adjust(const int32_t* __restrict__ disp, int32_t* __restrict__ out,
                          const uint8_t* __restrict__ edges, const float* __restrict__ vol0,
-                         DevParams P) {
+                         DevParams Pk) {
+    const DevParams P = Pk;  // kernel args -> registers once (no per-use kernarg reloads)
     const int x = blockIdx.x * blockDim.x + threadIdx.x;
     const int y = blockIdx.y;
     const int H = P.H, W = P.W, minD = P.minD, Lp = P.Lp;
@@ -519,7 +524,8 @@ __global__ void k_adjust(const int32_t* __restrict__ disp, int32_t* __restrict__
 
 // subpixelEnhancement (:1344-1370)
 __global__ void k_subpix(const int32_t* __restrict__ disp, const float* __restrict__ vol0,
-                         float* __restrict__ sub, DevParams P) {
+                         float* __restrict__ sub, DevParams Pk) {
+    const DevParams P = Pk;  // kernel args -> registers once (no per-use kernarg reloads)
     const int x = blockIdx.x * blockDim.x + threadIdx.x;
     const int y = blockIdx.y;
     const int W = P.W, minD = P.minD, Lp = P.Lp;
@@ -572,7 +578,8 @@ __global__ void k_median_out(const float* __restrict__ sub, float* __restrict__ 
 // ---------------------------------------------------------------------------
 // debug layout conversions
 // ---------------------------------------------------------------------------
-__global__ void k_vol_to_ref(const float* __restrict__ vol, float* __restrict__ ref, DevParams P) {
+__global__ void k_vol_to_ref(const float* __restrict__ vol, float* __restrict__ ref, DevParams Pk) {
+    const DevParams P = Pk;  // kernel args -> registers once (no per-use kernarg reloads)
     const size_t N = (size_t)P.H * P.W;
     const int v = blockIdx.z;
     const int d = blockIdx.y;
@@ -580,7 +587,8 @@ __global__ void k_vol_to_ref(const float* __restrict__ vol, float* __restrict__ 
         ref[((size_t)v * P.L + d) * N + i] = vol[((size_t)v * N + i) * P.Lp + d];
 }
 
-__global__ void k_arms_to_ref(const uint32_t* __restrict__ arms, int32_t* __restrict__ ref, DevParams P) {
+__global__ void k_arms_to_ref(const uint32_t* __restrict__ arms, int32_t* __restrict__ ref, DevParams Pk) {
+    const DevParams P = Pk;  // kernel args -> registers once (no per-use kernarg reloads)
     const size_t N = (size_t)P.H * P.W;
     const int v = blockIdx.y;
     for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < N; i += (size_t)gridDim.x * blockDim.x) {

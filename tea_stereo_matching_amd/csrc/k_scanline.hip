@@ -81,11 +81,26 @@ __device__ __forceinline__ int vec_argmin(const f32x4 (&x)[J], int lane, int Q, 
 // One partialOptimization step (ADCensus.cpp:869-913) for the wave's pixel p given its
 // predecessor q (registers).  g[j] packs the four d2 bytes (other-view colour difference,
 // or colorDiff+1 when out of range) of this lane's disparities.
+// Scalars the hot loop needs, pinned in SGPRs: an empty asm makes each value opaque,
+// so the compiler cannot rematerialise it from kernarg memory (a scalar load + lgkmcnt(0)
+// wait per use inside the serial loop).
+struct ScanConst {
+    int L, Q, cd, minD, W;
+    float p1[3], p2[3];
+};
+__device__ __forceinline__ ScanConst scan_const(const DevParams& P) {
+    ScanConst c{P.L, P.Lp >> 2, P.color_diff, P.minD, P.W,
+                {P.p1t[0], P.p1t[1], P.p1t[2]}, {P.p2t[0], P.p2t[1], P.p2t[2]}};
+    asm volatile("" : "+s"(c.L), "+s"(c.Q), "+s"(c.cd), "+s"(c.minD), "+s"(c.W));
+    asm volatile("" : "+s"(c.p1[0]), "+s"(c.p1[1]), "+s"(c.p1[2]), "+s"(c.p2[0]), "+s"(c.p2[1]), "+s"(c.p2[2]));
+    return c;
+}
+
 template <int J>
 __device__ __forceinline__ void partial_opt(f32x4 (&p)[J], const f32x4 (&q)[J], float mq, int d1,
-                                            const uint32_t (&g)[J], int lane, int Q, const DevParams& P) {
-    const int L = P.L;
-    const int cd = P.color_diff;
+                                            const uint32_t (&g)[J], int lane, const ScanConst& C) {
+    const int L = C.L, Q = C.Q;
+    const int cd = C.cd;
     const int s1 = d1 < cd ? 1 : 0;
 #pragma unroll
     for (int j = 0; j < J; ++j) {
@@ -110,8 +125,8 @@ __device__ __forceinline__ void partial_opt(f32x4 (&p)[J], const f32x4 (&q)[J], 
             if (d >= L) break;
             const int d2 = (g[j] >> (8 * k)) & 0xff;
             const int cnt = s1 + (d2 < cd ? 1 : 0);
-            const float p1 = cnt == 2 ? P.p1t[2] : (cnt == 1 ? P.p1t[1] : P.p1t[0]);
-            const float p2 = cnt == 2 ? P.p2t[2] : (cnt == 1 ? P.p2t[1] : P.p2t[0]);
+            const float p1 = cnt == 2 ? C.p1[2] : (cnt == 1 ? C.p1[1] : C.p1[0]);
+            const float p2 = cnt == 2 ? C.p2[2] : (cnt == 1 ? C.p2[1] : C.p2[0]);
             const float cost = pe[k] - mq;
             float mo = mq + p2;
             const float t0 = qe[k + 1];
@@ -150,8 +165,9 @@ struct LineStep {
 template <int J, bool HORIZ>
 __device__ __forceinline__ void scan_issue(LineStep<J, HORIZ>& st, int it, int n, int dir, int line,
                                            const float* base, size_t es, const uint8_t* gown,
-                                           const uint8_t* goth, int sgn, int lane, int Q,
-                                           const DevParams& P) {
+                                           const uint8_t* goth, int sgn, int lane,
+                                           const ScanConst& C) {
+    const int Q = C.Q;
     const int len = n + 1;
     const int pos = dir > 0 ? 1 + it : len - 2 - it;  // w1 (HORIZ) or h1 (vertical)
     const int pm = dir > 0 ? pos : pos + 1;            // max(pos, predecessor)
@@ -161,10 +177,14 @@ __device__ __forceinline__ void scan_issue(LineStep<J, HORIZ>& st, int it, int n
         const int q = lane + 64 * j;
         st.p[j] = q < Q ? *reinterpret_cast<const f32x4*>(ptr + 4 * q) : f32x4{0.f, 0.f, 0.f, 0.f};
     }
-    const int W = P.W;
-    const int cd1 = P.color_diff + 1;
+    const int W = C.W;
+    const int cd1 = C.cd + 1;
+    // d1's address is wave-uniform; a scalar load would need lgkmcnt(0) at its use and
+    // serialise the prefetch, so the index is moved to a VGPR to get an ordered vector load
+    int d1_idx = HORIZ ? pm : pm * W + line;
+    asm volatile("v_mov_b32 %0, %1" : "=v"(d1_idx) : "v"(d1_idx));
+    st.d1 = gown[d1_idx];
     if (HORIZ) {
-        st.d1 = gown[pm];
         const int off = dir > 0 ? 0 : 1;  // max(x1, x2) - x1
 #pragma unroll
         for (int j = 0; j < J; ++j) {
@@ -172,16 +192,15 @@ __device__ __forceinline__ void scan_issue(LineStep<J, HORIZ>& st, int it, int n
 #pragma unroll
             for (int e = 0; e < 4; ++e) {
                 const int d = 4 * (lane + 64 * j) + e;
-                const int x1 = pos + sgn * (d + P.minD);
+                const int x1 = pos + sgn * (d + C.minD);
                 const int x2 = x1 - dir;
-                const bool in = x1 >= 0 && x1 < W && x2 >= 0 && x2 < W && d < P.L;
+                const bool in = x1 >= 0 && x1 < W && x2 >= 0 && x2 < W && d < C.L;
                 const uint32_t b = in ? goth[x1 + off] : (uint32_t)cd1;
                 g |= b << (8 * e);
             }
             st.g[j] = g;
         }
     } else {
-        st.d1 = gown[(size_t)pm * W + line];
         const uint8_t* grow = goth + (size_t)pm * W;
 #pragma unroll
         for (int j = 0; j < J; ++j) {
@@ -189,8 +208,8 @@ __device__ __forceinline__ void scan_issue(LineStep<J, HORIZ>& st, int it, int n
 #pragma unroll
             for (int e = 0; e < 4; ++e) {
                 const int d = 4 * (lane + 64 * j) + e;
-                const int x = line + sgn * (d + P.minD);
-                const uint32_t b = (x >= 0 && x < W && d < P.L) ? grow[x] : (uint32_t)cd1;
+                const int x = line + sgn * (d + C.minD);
+                const uint32_t b = (x >= 0 && x < W && d < C.L) ? grow[x] : (uint32_t)cd1;
                 g |= b << (8 * e);
             }
             st.g[j] = g;
@@ -203,7 +222,8 @@ __global__ __launch_bounds__(256) void k_scan_line(float* __restrict__ vol,
                                                    const uint8_t* __restrict__ grad,
                                                    const uint32_t* __restrict__ img, int dir,
                                                    int32_t* __restrict__ wta, int store_view1,
-                                                   DevParams P) {
+                                                   DevParams Pk) {
+    const DevParams P = Pk;  // kernel args -> registers once (no per-use kernarg reloads)
     const int H = P.H, W = P.W, Lp = P.Lp, Q = Lp >> 2;
     const int lane = threadIdx.x & 63;
     const int line = __builtin_amdgcn_readfirstlane(blockIdx.x * 4 + (threadIdx.x >> 6));
@@ -220,6 +240,7 @@ __global__ __launch_bounds__(256) void k_scan_line(float* __restrict__ vol,
     const int T = P.omp_threads;
     const bool store = !(wta && v == 1 && !store_view1);
     int32_t* wrow = wta ? wta + ((size_t)v * H + line) * W : nullptr;  // only HORIZ passes emit WTA
+    const ScanConst C = scan_const(P);
 
     f32x4 q[J];
     const int p0 = dir > 0 ? 0 : len - 1;
@@ -241,7 +262,7 @@ __global__ __launch_bounds__(256) void k_scan_line(float* __restrict__ vol,
     LineStep<J, HORIZ> ring[SC_K];
 #pragma unroll
     for (int k = 0; k < SC_K; ++k)
-        if (k < n) scan_issue<J, HORIZ>(ring[k], k, n, dir, line, base, es, gown, goth, sgn, lane, Q, P);
+        if (k < n) scan_issue<J, HORIZ>(ring[k], k, n, dir, line, base, es, gown, goth, sgn, lane, C);
 
     for (int b = 0; b < n; b += SC_K) {
 #pragma unroll
@@ -254,7 +275,7 @@ __global__ __launch_bounds__(256) void k_scan_line(float* __restrict__ vol,
                 for (int j = 0; j < J; ++j) { p[j] = ring[k].p[j]; g[j] = ring[k].g[j]; }
                 const int d1 = ring[k].d1;
                 if (it + SC_K < n)
-                    scan_issue<J, HORIZ>(ring[k], it + SC_K, n, dir, line, base, es, gown, goth, sgn, lane, Q, P);
+                    scan_issue<J, HORIZ>(ring[k], it + SC_K, n, dir, line, base, es, gown, goth, sgn, lane, C);
                 const int pos = dir > 0 ? 1 + it : len - 2 - it;
                 const int pred = pos - dir;
                 if (T > 1 && omp_chunk_start(it, n, T)) {  // stale predecessor (racy schedule)
@@ -266,11 +287,11 @@ __global__ __launch_bounds__(256) void k_scan_line(float* __restrict__ vol,
                 if (keep) {
 #pragma unroll
                     for (int j = 0; j < J; ++j) qorig[j] = p[j];
-                    mqorig = vec_min<J>(p, lane, Q, P.L);
+                    mqorig = vec_min<J>(p, lane, C.Q, C.L);
                 }
                 const bool masked = P.mask && (HORIZ ? im[(size_t)line * W + pred] : im[(size_t)pred * W + line]) == 0;
                 if (!(masked || mq == 0.f)) {  // :880-881 -- else p stays untouched
-                    partial_opt<J>(p, q, mq, d1, g, lane, Q, P);
+                    partial_opt<J>(p, q, mq, d1, g, lane, C);
                     if (store) {
 #pragma unroll
                         for (int j = 0; j < J; ++j) {
@@ -281,9 +302,9 @@ __global__ __launch_bounds__(256) void k_scan_line(float* __restrict__ vol,
                 }
 #pragma unroll
                 for (int j = 0; j < J; ++j) q[j] = p[j];
-                mq = vec_min<J>(q, lane, Q, P.L);
+                mq = vec_min<J>(q, lane, C.Q, C.L);
                 if (wrow) {
-                    const int d = vec_argmin<J>(q, lane, Q, P.L, P.minD, mq);
+                    const int d = vec_argmin<J>(q, lane, C.Q, C.L, C.minD, mq);
                     if (lane == 0) wrow[pos] = d;
                 }
             }
