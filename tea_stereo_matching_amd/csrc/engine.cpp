@@ -82,7 +82,7 @@ void default_params(tsm_adc_params* p, int model) {
 
 struct Workspace {
     hipStream_t stream = nullptr;
-    int H = 0, W = 0, L = 0, Lp = 0, model = -1;
+    int H = 0, W = 0, L = 0, Lp = 0, model = -1, maxD = -1;
     float lambda_ad = 0, lambda_census = 0;
     size_t bytes = 0;
     // host-API staging
@@ -98,8 +98,8 @@ struct Workspace {
     float* vol = nullptr;          // [2][H][W][Lp]
     uint32_t* arms = nullptr;      // [2][H][W]
     int32_t* ws = nullptr;         // [2][2][H][W]
-    uint8_t* gv = nullptr;         // [2][H][W]
-    uint8_t* gh = nullptr;         // [2][H][W]
+    uint8_t* gv = nullptr;         // [2][H][gstride] (sentinel margins)
+    uint8_t* gh = nullptr;         // [2][H][gstride]
     float* lutA = nullptr;
     float* lutB = nullptr;
     int lutA_n = 0;
@@ -172,7 +172,7 @@ size_t workspace_bytes(int H, int W, int L) {
     b += 2 * N * Lp * 4;       // vol
     b += 2 * N * 4;            // arms
     b += 4 * N * 4;            // ws
-    b += 4 * N;                // gv, gh
+    b += 4 * (size_t)H * (W + 2 * grad_pad(L) + 16);  // gv, gh (upper bound)
     b += N * (4 * 8 + 2 * 20 + 1 * 6 + 2 * 2 + 4); // refine maps
     return b;
 }
@@ -246,6 +246,8 @@ DevParams make_params(const tsm_adc* h, int H, int W) {
     P.canny_low = (int)std::floor(lo);
     P.canny_high = (int)std::floor(hi);
     P.omp_threads = h->omp_threads;
+    P.gpad = grad_pad(P.maxD);
+    P.gstride = ((W + 2 * P.gpad + 15) / 16) * 16;
     return P;
 }
 
@@ -253,7 +255,7 @@ int ensure_workspace(tsm_adc* h, Workspace* w, int H, int W) {
     const int L = h->max_disparity - h->min_disparity + 1;
     if (w->stream == nullptr) HIP_OK(hipStreamCreateWithFlags(&w->stream, hipStreamNonBlocking));
     const tsm_adc_params& p = h->params;
-    if (w->H == H && w->W == W && w->L == L && w->model == h->color_model &&
+    if (w->H == H && w->W == W && w->L == L && w->maxD == h->max_disparity && w->model == h->color_model &&
         w->lambda_ad == p.lambda_ad && w->lambda_census == p.lambda_census)
         return TSM_OK;
     HIP_OK(hipStreamSynchronize(w->stream));
@@ -274,8 +276,12 @@ int ensure_workspace(tsm_adc* h, Workspace* w, int H, int W) {
     A(w->vol, 2 * N * (size_t)Lp * 4);
     A(w->arms, 2 * N * 4);
     A(w->ws, 4 * N * 4);
-    A(w->gv, 2 * N);
-    A(w->gh, 2 * N);
+    {
+        const int gp = grad_pad(h->max_disparity);
+        const size_t gs = (size_t)(((W + 2 * gp + 15) / 16) * 16);
+        A(w->gv, 2 * (size_t)H * gs + 64);
+        A(w->gh, 2 * (size_t)H * gs + 64);
+    }
     RefineBufs& B = w->rb;
     A(B.disp0, 2 * N * 4);  // [2][H][W]: the fused WTA writes view v at disp0 + v*N
     B.disp1 = B.disp0 + N;
@@ -315,6 +321,7 @@ int ensure_workspace(tsm_adc* h, Workspace* w, int H, int W) {
     w->W = W;
     w->L = L;
     w->Lp = Lp;
+    w->maxD = h->max_disparity;
     w->model = h->color_model;
     w->lambda_ad = p.lambda_ad;
     w->lambda_census = p.lambda_census;

@@ -107,21 +107,31 @@ __global__ void k_window_sizes(const uint32_t* __restrict__ arms, int32_t* __res
 
 // colour differences between vertical / horizontal neighbours of each view image,
 // used by the scanline P1/P2 rule (computeP1P2, :915-981; colorDiff is symmetric):
-//   gv[v][y][x] = colorDiff(img_v(y,x), img_v(y-1,x))  (y >= 1)
-//   gh[v][y][x] = colorDiff(img_v(y,x), img_v(y,x-1))  (x >= 1)
+//   gv[v][y][gpad + x] = colorDiff(img_v(y,x), img_v(y-1,x))  (y >= 1)
+//   gh[v][y][gpad + x] = colorDiff(img_v(y,x), img_v(y,x-1))  (x >= 1)
+// Every byte outside those ranges (margins, x = 0 for gh, y = 0 for gv) holds the
+// sentinel colorDiff+1, which is exactly the reference's out-of-image value of d2
+// (:928), so the scanline reads the maps without range checks.
 __global__ void k_color_grad(const uint32_t* __restrict__ img, uint8_t* __restrict__ gv,
                              uint8_t* __restrict__ gh, DevParams Pk) {
-    const DevParams P = Pk;  // kernel args -> registers once (no per-use kernarg reloads)
-    const int x = blockIdx.x * blockDim.x + threadIdx.x;
+    const DevParams P = Pk;
+    const int xs = blockIdx.x * blockDim.x + threadIdx.x;
     const int y = blockIdx.y;
     const int v = blockIdx.z;
     const int H = P.H, W = P.W;
-    if (x >= W) return;
+    if (xs >= P.gstride) return;
+    const int x = xs - P.gpad;
+    const uint8_t sent = (uint8_t)(P.color_diff + 1);
     const uint32_t* im = img + (size_t)v * H * W;
-    const uint32_t c = im[(size_t)y * W + x];
-    const size_t o = ((size_t)v * H + y) * W + x;
-    gv[o] = (uint8_t)(y >= 1 ? color_diff(P, c, im[(size_t)(y - 1) * W + x]) : 0);
-    gh[o] = (uint8_t)(x >= 1 ? color_diff(P, c, im[(size_t)y * W + (x - 1)]) : 0);
+    const size_t o = ((size_t)v * H + y) * P.gstride + xs;
+    uint8_t a = sent, b = sent;
+    if (x >= 0 && x < W) {
+        const uint32_t c = im[(size_t)y * W + x];
+        if (y >= 1) a = (uint8_t)color_diff(P, c, im[(size_t)(y - 1) * W + x]);
+        if (x >= 1) b = (uint8_t)color_diff(P, c, im[(size_t)y * W + (x - 1)]);
+    }
+    gv[o] = a;
+    gh[o] = b;
 }
 
 // ---------------------------------------------------------------------------
@@ -265,7 +275,7 @@ void launch_window_sizes(const uint32_t* arms, int32_t* ws, const DevParams& P, 
 
 void launch_color_grad(const uint32_t* img, uint8_t* gv, uint8_t* gh, const DevParams& P,
                        hipStream_t st) {
-    dim3 g((P.W + 255) / 256, P.H, 2);
+    dim3 g((P.gstride + 255) / 256, P.H, 2);
     hipLaunchKernelGGL(k_color_grad, g, dim3(256), 0, st, img, gv, gh, P); trace_point("k_color_grad", st);
 }
 

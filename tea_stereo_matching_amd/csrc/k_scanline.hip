@@ -7,10 +7,21 @@
 // already-updated L-vector.  The reference parallelises each pass over the recursion
 // dimension (a data race); the kernels implement the serial semantics: one wave owns one
 // line (a column for the vertical passes, a row for the horizontal ones) and walks it,
-// keeping the predecessor vector in registers (lanes own 4 consecutive disparities), so
-// the min over disparities is a wave reduction and the d+-1 neighbours are DPP lane
-// shifts.  Optional emulation of the race's lock-step outcome for T threads: the first
-// pixel of each of the T static chunks reads its predecessor's pre-pass vector.
+// keeping the predecessor vector in registers (lanes own 4 consecutive disparities).
+//
+// The walk is serial, with under one wave per SIMD, so the cost of a step is its
+// instruction count.  The step is kept branch-free and short:
+//  * the padding disparities d >= L of every vector hold +inf (written by the cost
+//    kernel, preserved by aggregation and by this update), so the d-1 / d+1 neighbours
+//    of d = 0 and d = L-1 need no guards: +inf never wins a min;
+//  * all values are non-negative floats, which order like their bit patterns, so every
+//    min is an unsigned-integer v_min3_u32 (exact, no canonicalisation);
+//  * d2 (the other view's colour difference, or colorDiff+1 out of range) comes from a
+//    sentinel-padded byte map through one aligned 8-byte load + v_alignbyte per step;
+//  * everything that does not depend on the chain (the pixel vector, d1, the d2 bytes)
+//    is prefetched SC_K steps ahead into a register ring.
+// Optional emulation of the reference's racy omp-static schedule for T threads: the
+// first pixel of each of the T chunks reads its predecessor's pre-pass vector.
 #include "tsm_device.h"
 #include "tsm_launch.h"
 
@@ -20,8 +31,7 @@ namespace tsm {
 __device__ __forceinline__ bool omp_chunk_start(int it, int n, int T) {
     if (T <= 1 || n <= 0 || it == 0) return false;
     const int q = n / T, r = n % T;
-    // chunk t starts at t*q + min(t, r)
-    if (q == 0) return it < r; // every thread owns one iteration
+    if (q == 0) return it < r;  // every thread owns one iteration
     int t;
     if (it < r * (q + 1)) {
         if (it % (q + 1) != 0) return false;
@@ -34,188 +44,178 @@ __device__ __forceinline__ bool omp_chunk_start(int it, int n, int T) {
     return t > 0 && t < T;
 }
 
+constexpr uint32_t kInfBits = 0x7f800000u;
+
+__device__ __forceinline__ uint32_t fbits(float x) { return __float_as_uint(x); }
+__device__ __forceinline__ float bitsf(uint32_t x) { return __uint_as_float(x); }
+__device__ __forceinline__ uint32_t umin3(uint32_t a, uint32_t b, uint32_t c) {
+    return min(min(a, b), c);  // lowered to v_min3_u32
+}
+
+// wave min of non-negative floats held as bits (+inf padding is neutral)
 template <int J>
-__device__ __forceinline__ float vec_min(const f32x4 (&x)[J], int lane, int Q, int L, int from = 0) {
-    float m = __int_as_float(0x7f800000);
+__device__ __forceinline__ uint32_t vec_min_bits(const f32x4 (&x)[J]) {
+    uint32_t m = min(min(fbits(x[0][0]), fbits(x[0][1])), min(fbits(x[0][2]), fbits(x[0][3])));
 #pragma unroll
-    for (int j = 0; j < J; ++j) {
-        const int q = lane + 64 * j;
-        if (q < Q) {
-            const int d = 4 * q;
-#pragma unroll
-            for (int e = 0; e < 4; ++e)
-                if (d + e < L && d + e >= from) m = fminf(m, x[j][e]);
-        }
-    }
-    return wave_min_nonneg(m);
+    for (int j = 1; j < J; ++j)
+        m = min(m, min(min(fbits(x[j][0]), fbits(x[j][1])), min(fbits(x[j][2]), fbits(x[j][3]))));
+    return __float_as_uint(wave_min_nonneg(bitsf(m)));
 }
 
 // WTA over indices [minD, L-1], first minimum (strict <, ADCensus.cpp:1404): the first d
-// whose cost equals the wave minimum, found by a ballot (no 64-bit shuffle reduction).
-// `m` is the wave min over [0, L); recomputed over [minD, L) when minD > 0.
+// whose cost equals the minimum, found by a ballot.
 template <int J>
-__device__ __forceinline__ int vec_argmin(const f32x4 (&x)[J], int lane, int Q, int L, int minD, float m) {
-    if (minD > 0) m = vec_min<J>(x, lane, Q, L, minD);
-    if (!(m < 3.402823466e+38f)) return minD;  // nothing below FLT_MAX: reference leaves it unset
+__device__ __forceinline__ int vec_argmin(const f32x4 (&x)[J], int lane, int L, int minD, uint32_t m) {
+    if (minD > 0) {  // minimum over [minD, L) only
+        uint32_t mm = ~0u;
+#pragma unroll
+        for (int j = 0; j < J; ++j)
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+                const int d = 4 * (lane + 64 * j) + e;
+                if (d >= minD) mm = min(mm, fbits(x[j][e]));
+            }
+        m = __float_as_uint(wave_min_nonneg(bitsf(mm)));
+    }
+    if (!(bitsf(m) < 3.402823466e+38f)) return minD;  // nothing below FLT_MAX (reference: unset)
 #pragma unroll
     for (int j = 0; j < J; ++j) {
-        const int q = lane + 64 * j;
         int first = 4;
-        if (q < Q) {
 #pragma unroll
-            for (int e = 3; e >= 0; --e) {
-                const int d = 4 * q + e;
-                if (d < L && d >= minD && x[j][e] == m) first = e;
-            }
+        for (int e = 3; e >= 0; --e) {
+            const int d = 4 * (lane + 64 * j) + e;
+            if (fbits(x[j][e]) == m && d >= minD && d < L) first = e;
         }
         const uint64_t mask = __ballot(first < 4);
         if (mask) {
             const int ln = __builtin_ctzll(mask);
-            const int e = __builtin_amdgcn_readlane(first, ln);
-            return 4 * (ln + 64 * j) + e;
+            return 4 * (ln + 64 * j) + __builtin_amdgcn_readlane(first, ln);
         }
     }
     return minD;
 }
 
-// One partialOptimization step (ADCensus.cpp:869-913) for the wave's pixel p given its
-// predecessor q (registers).  g[j] packs the four d2 bytes (other-view colour difference,
-// or colorDiff+1 when out of range) of this lane's disparities.
-// Scalars the hot loop needs, pinned in SGPRs: an empty asm makes each value opaque,
-// so the compiler cannot rematerialise it from kernarg memory (a scalar load + lgkmcnt(0)
-// wait per use inside the serial loop).
+// Hot-loop scalars, pinned in SGPRs (an empty asm makes each value opaque, so the
+// compiler cannot rematerialise it from kernarg memory inside the serial loop).
 struct ScanConst {
-    int L, Q, cd, minD, W;
+    int L, Q, cd, minD, W, gstride, gpad;
     float p1[3], p2[3];
 };
 __device__ __forceinline__ ScanConst scan_const(const DevParams& P) {
-    ScanConst c{P.L, P.Lp >> 2, P.color_diff, P.minD, P.W,
+    ScanConst c{P.L, P.Lp >> 2, P.color_diff, P.minD, P.W, P.gstride, P.gpad,
                 {P.p1t[0], P.p1t[1], P.p1t[2]}, {P.p2t[0], P.p2t[1], P.p2t[2]}};
-    asm volatile("" : "+s"(c.L), "+s"(c.Q), "+s"(c.cd), "+s"(c.minD), "+s"(c.W));
+    asm volatile("" : "+s"(c.L), "+s"(c.Q), "+s"(c.cd), "+s"(c.minD), "+s"(c.W), "+s"(c.gstride), "+s"(c.gpad));
     asm volatile("" : "+s"(c.p1[0]), "+s"(c.p1[1]), "+s"(c.p1[2]), "+s"(c.p2[0]), "+s"(c.p2[1]), "+s"(c.p2[2]));
     return c;
 }
 
+// Prefetched, chain-independent inputs of one step.
 template <int J>
-__device__ __forceinline__ void partial_opt(f32x4 (&p)[J], const f32x4 (&q)[J], float mq, int d1,
-                                            const uint32_t (&g)[J], int lane, const ScanConst& C) {
-    const int L = C.L, Q = C.Q;
-    const int cd = C.cd;
-    const int s1 = d1 < cd ? 1 : 0;
-#pragma unroll
-    for (int j = 0; j < J; ++j) {
-        // neighbours across the float4 boundary: d-1 of element 0, d+1 of element 3
-        float lo = dpp_f<DPP_WAVE_SHR1>(q[j][3], 0.f);
-        float hi = dpp_f<DPP_WAVE_SHL1>(q[j][0], 0.f);
-        if (j > 0) {
-            const float prev = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(q[j - 1][3]), 63));
-            if (lane == 0) lo = prev;
-        }
-        if (j + 1 < J) {
-            const float nxt = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(q[j + 1][0]), 0));
-            if (lane == 63) hi = nxt;
-        }
-        const int qi = lane + 64 * j;
-        if (qi >= Q) continue;
-        const float qe[6] = {lo, q[j][0], q[j][1], q[j][2], q[j][3], hi};
-        f32x4 pe = p[j];
-#pragma unroll
-        for (int k = 0; k < 4; ++k) {
-            const int d = 4 * qi + k;
-            if (d >= L) break;
-            const int d2 = (g[j] >> (8 * k)) & 0xff;
-            const int cnt = s1 + (d2 < cd ? 1 : 0);
-            const float p1 = cnt == 2 ? C.p1[2] : (cnt == 1 ? C.p1[1] : C.p1[0]);
-            const float p2 = cnt == 2 ? C.p2[2] : (cnt == 1 ? C.p2[1] : C.p2[0]);
-            const float cost = pe[k] - mq;
-            float mo = mq + p2;
-            const float t0 = qe[k + 1];
-            if (mo > t0) mo = t0;
-            if (d != 0) {
-                const float t = qe[k] + p1;
-                if (mo > t) mo = t;
-            }
-            if (d != L - 1) {
-                const float t = qe[k + 2] + p1;
-                if (mo > t) mo = t;
-            }
-            pe[k] = (cost + mo) / 2;
-        }
-        p[j] = pe;
-    }
-}
-
-// ---------------------------------------------------------------------------
-// One wave walks one line (a column for vertical passes, a row for horizontal ones) of
-// one view.  Everything a step needs that does not depend on the chain -- the pixel's
-// L-vector, the uniform d1 and the per-disparity d2 bytes -- is prefetched K steps ahead
-// into a register ring, so the serial critical path is only the update + wave min.
-// The leftward horizontal pass is the last one: it emits the WTA disparity of every
-// pixel and, for view 1 (only needed for the WTA), can skip storing the volume.
-// ---------------------------------------------------------------------------
-constexpr int SC_K = 8;  // prefetch depth (steps)
-
-template <int J, bool HORIZ>
-struct LineStep {
-    f32x4 p[J];
-    uint32_t g[J];
-    int d1;
+struct StepIn {
+    f32x4 p[J];      // this pixel's L-vector (padding and lanes >= Q: +inf)
+    uint32_t g0[J];  // aligned 8-byte window of the other view's colour differences
+    uint32_t g1[J];
+    int d1;          // own-view colour difference to the predecessor
+    uint32_t mk;     // mask mode: predecessor's packed colour (0 = black)
 };
 
+// d2 bytes of this lane's 4 disparities from the 8-byte window: view 0 reads x ascending,
+// view 1 descending (x = pos -/+ (d + minD)), so view 1 byte-reverses.
+__device__ __forceinline__ uint32_t d2_bytes(uint32_t lo, uint32_t hi, uint32_t sh, bool rev) {
+    const uint32_t w = __builtin_amdgcn_alignbyte(hi, lo, sh);
+    return rev ? __builtin_amdgcn_perm(w, w, 0x00010203u) : w;
+}
+
 template <int J, bool HORIZ>
-__device__ __forceinline__ void scan_issue(LineStep<J, HORIZ>& st, int it, int n, int dir, int line,
+__device__ __forceinline__ void scan_issue(StepIn<J>& s, int it, int len, int dir, int line,
                                            const float* base, size_t es, const uint8_t* gown,
-                                           const uint8_t* goth, int sgn, int lane,
-                                           const ScanConst& C) {
-    const int Q = C.Q;
-    const int len = n + 1;
+                                           const uint8_t* goth, const uint32_t* im, bool mask,
+                                           int sgn, int lane, const ScanConst& C) {
     const int pos = dir > 0 ? 1 + it : len - 2 - it;  // w1 (HORIZ) or h1 (vertical)
     const int pm = dir > 0 ? pos : pos + 1;            // max(pos, predecessor)
     const float* ptr = base + (size_t)pos * es;
 #pragma unroll
     for (int j = 0; j < J; ++j) {
         const int q = lane + 64 * j;
-        st.p[j] = q < Q ? *reinterpret_cast<const f32x4*>(ptr + 4 * q) : f32x4{0.f, 0.f, 0.f, 0.f};
+        const int qc = q < C.Q ? q : C.Q - 1;  // clamped, always-valid address
+        const f32x4 v = *reinterpret_cast<const f32x4*>(ptr + 4 * qc);
+        const float inf = bitsf(kInfBits);
+        s.p[j] = q < C.Q ? v : f32x4{inf, inf, inf, inf};
     }
-    const int W = C.W;
-    const int cd1 = C.cd + 1;
-    // d1's address is wave-uniform; a scalar load would need lgkmcnt(0) at its use and
-    // serialise the prefetch, so the index is moved to a VGPR to get an ordered vector load
-    int d1_idx = HORIZ ? pm : pm * W + line;
-    asm volatile("v_mov_b32 %0, %1" : "=v"(d1_idx) : "v"(d1_idx));
-    st.d1 = gown[d1_idx];
-    if (HORIZ) {
-        const int off = dir > 0 ? 0 : 1;  // max(x1, x2) - x1
+    // d1 / mask loads: wave-uniform addresses laundered into a VGPR, so they are
+    // vector loads ordered by vmcnt (a scalar load would need lgkmcnt(0) at its use)
+    int i1 = HORIZ ? C.gpad + pm : pm * C.gstride + C.gpad + line;
+    asm volatile("v_mov_b32 %0, %1" : "=v"(i1) : "v"(i1));
+    s.d1 = gown[i1];
+    s.mk = 1u;
+    if (mask) {
+        int im_idx = HORIZ ? line * C.W + (pos - dir) : (pos - dir) * C.W + line;
+        asm volatile("v_mov_b32 %0, %1" : "=v"(im_idx) : "v"(im_idx));
+        s.mk = im[im_idx];
+    }
+    // x of this lane's first disparity; HORIZ reads byte max(x1, x2) = x1 + (dir < 0)
+    const uint8_t* grow = HORIZ ? goth : goth + (size_t)pm * C.gstride;
+    const int x0 = (HORIZ ? pos + (dir < 0 ? 1 : 0) : line) + C.gpad + sgn * C.minD;
 #pragma unroll
-        for (int j = 0; j < J; ++j) {
-            uint32_t g = 0;
-#pragma unroll
-            for (int e = 0; e < 4; ++e) {
-                const int d = 4 * (lane + 64 * j) + e;
-                const int x1 = pos + sgn * (d + C.minD);
-                const int x2 = x1 - dir;
-                const bool in = x1 >= 0 && x1 < W && x2 >= 0 && x2 < W && d < C.L;
-                const uint32_t b = in ? goth[x1 + off] : (uint32_t)cd1;
-                g |= b << (8 * e);
-            }
-            st.g[j] = g;
-        }
-    } else {
-        const uint8_t* grow = goth + (size_t)pm * W;
-#pragma unroll
-        for (int j = 0; j < J; ++j) {
-            uint32_t g = 0;
-#pragma unroll
-            for (int e = 0; e < 4; ++e) {
-                const int d = 4 * (lane + 64 * j) + e;
-                const int x = line + sgn * (d + C.minD);
-                const uint32_t b = (x >= 0 && x < W && d < C.L) ? grow[x] : (uint32_t)cd1;
-                g |= b << (8 * e);
-            }
-            st.g[j] = g;
-        }
+    for (int j = 0; j < J; ++j) {
+        // bytes [b, b+4): view 0 b = x0 + 4q, view 1 b = x0 - 4q - 3 (then reversed)
+        const int q = lane + 64 * j;
+        const int b = sgn > 0 ? x0 + 4 * q : x0 - 4 * q - 3;
+        const int bc = b < 0 ? 0 : (b > C.gstride - 8 ? C.gstride - 8 : b);  // lanes past the vector
+        const uint2 w = *reinterpret_cast<const uint2*>(grow + (bc & ~3));
+        s.g0[j] = w.x;
+        s.g1[j] = w.y;
     }
 }
+
+// One partialOptimization step (ADCensus.cpp:869-913), branch-free.
+template <int J>
+__device__ __forceinline__ void partial_opt(f32x4 (&p)[J], const f32x4 (&q)[J], uint32_t mq,
+                                            int d1, const StepIn<J>& s, uint32_t sh, bool rev,
+                                            int lane, const ScanConst& C) {
+    const float mqf = bitsf(mq);
+    // P1/P2 pairs by d1 class (:954-979): d2 similar -> a, dissimilar -> b
+    const bool sim1 = d1 < C.cd;
+    const float p1a = sim1 ? C.p1[2] : C.p1[1], p1b = sim1 ? C.p1[1] : C.p1[0];
+    const float p2a = sim1 ? C.p2[2] : C.p2[1], p2b = sim1 ? C.p2[1] : C.p2[0];
+    const float inf = bitsf(kInfBits);
+#pragma unroll
+    for (int j = 0; j < J; ++j) {
+        // d-1 of element 0 / d+1 of element 3 from the neighbouring lanes (+inf at the ends)
+        float lo = dpp_f<DPP_WAVE_SHR1>(q[j][3], inf);
+        float hi = dpp_f<DPP_WAVE_SHL1>(q[j][0], inf);
+        if (j > 0) {
+            const float prev = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(q[j - 1][3]), 63));
+            lo = lane == 0 ? prev : lo;
+        }
+        if (j + 1 < J) {
+            const float nxt = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(q[j + 1][0]), 0));
+            hi = lane == 63 ? nxt : hi;
+        }
+        const uint32_t g = d2_bytes(s.g0[j], s.g1[j], sh, rev);
+        const float qe[6] = {lo, q[j][0], q[j][1], q[j][2], q[j][3], hi};
+        f32x4 pe = p[j];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const bool sim2 = (int)((g >> (8 * k)) & 0xffu) < C.cd;
+            const float p1 = sim2 ? p1a : p1b;
+            const float p2 = sim2 ? p2a : p2b;
+            const float cost = pe[k] - mqf;
+            // min{ m + P2, C(q,d), C(q,d-1) + P1, C(q,d+1) + P1 } (all >= 0: integer min)
+            const uint32_t mo = umin3(min(fbits(mqf + p2), fbits(qe[k + 1])), fbits(qe[k] + p1),
+                                      fbits(qe[k + 2] + p1));
+            pe[k] = (cost + bitsf(mo)) * 0.5f;  // == / 2 exactly
+        }
+        p[j] = pe;
+    }
+}
+
+// ---------------------------------------------------------------------------
+// One wave walks one line of one view.  The leftward horizontal pass is the last one:
+// it emits the WTA disparity of every pixel and, for view 1 (only needed for the WTA),
+// can skip storing the volume.
+// ---------------------------------------------------------------------------
+constexpr int SC_K = 8;  // prefetch depth (steps)
 
 template <int J, bool HORIZ>
 __global__ __launch_bounds__(256) void k_scan_line(float* __restrict__ vol,
@@ -223,88 +223,91 @@ __global__ __launch_bounds__(256) void k_scan_line(float* __restrict__ vol,
                                                    const uint32_t* __restrict__ img, int dir,
                                                    int32_t* __restrict__ wta, int store_view1,
                                                    DevParams Pk) {
-    const DevParams P = Pk;  // kernel args -> registers once (no per-use kernarg reloads)
-    const int H = P.H, W = P.W, Lp = P.Lp, Q = Lp >> 2;
+    const DevParams P = Pk;
+    const int H = P.H, W = P.W, Lp = P.Lp;
     const int lane = threadIdx.x & 63;
     const int line = __builtin_amdgcn_readfirstlane(blockIdx.x * 4 + (threadIdx.x >> 6));
     const int v = blockIdx.y;
     if (line >= (HORIZ ? H : W)) return;
+    const ScanConst C = scan_const(P);
     const int len = HORIZ ? W : H;
     const size_t es = HORIZ ? (size_t)Lp : (size_t)W * Lp;
     float* base = vol + (size_t)v * H * W * Lp + (HORIZ ? (size_t)line * W * Lp : (size_t)line * Lp);
-    const uint8_t* gown = grad + (size_t)v * H * W + (HORIZ ? (size_t)line * W : 0);
-    const uint8_t* goth = grad + (size_t)(1 - v) * H * W + (HORIZ ? (size_t)line * W : 0);
+    const uint8_t* gown = grad + (size_t)v * H * C.gstride + (HORIZ ? (size_t)line * C.gstride : 0);
+    const uint8_t* goth = grad + (size_t)(1 - v) * H * C.gstride + (HORIZ ? (size_t)line * C.gstride : 0);
     const uint32_t* im = img + (size_t)v * H * W;
+    const bool mask = P.mask != 0;
     const int sgn = v == 0 ? 1 : -1;
+    const bool rev = sgn < 0;
     const int n = len - 1;
     const int T = P.omp_threads;
     const bool store = !(wta && v == 1 && !store_view1);
     int32_t* wrow = wta ? wta + ((size_t)v * H + line) * W : nullptr;  // only HORIZ passes emit WTA
-    const ScanConst C = scan_const(P);
+    // byte misalignment of every lane's d2 window (uniform: lanes differ by multiples of 4)
+    const int x0a = (HORIZ ? (dir < 0 ? 1 : 0) : line) + C.gpad + sgn * C.minD - (sgn > 0 ? 0 : 3);
+    const int posbase = dir > 0 ? 1 : len - 2;  // pos(it) = posbase + dir*it (HORIZ shifts x0)
 
     f32x4 q[J];
     const int p0 = dir > 0 ? 0 : len - 1;
 #pragma unroll
     for (int j = 0; j < J; ++j) {
         const int qq = lane + 64 * j;
-        q[j] = qq < Q ? *reinterpret_cast<const f32x4*>(base + (size_t)p0 * es + 4 * qq) : f32x4{0.f, 0.f, 0.f, 0.f};
+        const int qc = qq < C.Q ? qq : C.Q - 1;
+        const f32x4 v0 = *reinterpret_cast<const f32x4*>(base + (size_t)p0 * es + 4 * qc);
+        const float inf = bitsf(kInfBits);
+        q[j] = qq < C.Q ? v0 : f32x4{inf, inf, inf, inf};
     }
-    float mq = vec_min<J>(q, lane, Q, P.L);
+    uint32_t mq = vec_min_bits<J>(q);
     if (wrow) {
-        const int d = vec_argmin<J>(q, lane, Q, P.L, P.minD, mq);
+        const int d = vec_argmin<J>(q, lane, C.L, C.minD, mq);
         if (lane == 0) wrow[p0] = d;
     }
     f32x4 qorig[J];
-    float mqorig = mq;
+    uint32_t mqorig = mq;
 #pragma unroll
     for (int j = 0; j < J; ++j) qorig[j] = q[j];
 
-    LineStep<J, HORIZ> ring[SC_K];
+    StepIn<J> ring[SC_K];
 #pragma unroll
     for (int k = 0; k < SC_K; ++k)
-        if (k < n) scan_issue<J, HORIZ>(ring[k], k, n, dir, line, base, es, gown, goth, sgn, lane, C);
+        if (k < n) scan_issue<J, HORIZ>(ring[k], k, len, dir, line, base, es, gown, goth, im, mask, sgn, lane, C);
 
     for (int b = 0; b < n; b += SC_K) {
 #pragma unroll
         for (int k = 0; k < SC_K; ++k) {
             const int it = b + k;
             if (it < n) {
-                f32x4 p[J];
-                uint32_t g[J];
-#pragma unroll
-                for (int j = 0; j < J; ++j) { p[j] = ring[k].p[j]; g[j] = ring[k].g[j]; }
-                const int d1 = ring[k].d1;
+                StepIn<J> s = ring[k];
                 if (it + SC_K < n)
-                    scan_issue<J, HORIZ>(ring[k], it + SC_K, n, dir, line, base, es, gown, goth, sgn, lane, C);
-                const int pos = dir > 0 ? 1 + it : len - 2 - it;
-                const int pred = pos - dir;
+                    scan_issue<J, HORIZ>(ring[k], it + SC_K, len, dir, line, base, es, gown, goth, im, mask, sgn, lane, C);
+                const int pos = posbase + dir * it;
+                const uint32_t sh = (uint32_t)((HORIZ ? x0a + pos : x0a) & 3);
                 if (T > 1 && omp_chunk_start(it, n, T)) {  // stale predecessor (racy schedule)
 #pragma unroll
                     for (int j = 0; j < J; ++j) q[j] = qorig[j];
                     mq = mqorig;
                 }
-                const bool keep = T > 1 && omp_chunk_start(it + 1, n, T);
-                if (keep) {
+                if (T > 1 && omp_chunk_start(it + 1, n, T)) {
 #pragma unroll
-                    for (int j = 0; j < J; ++j) qorig[j] = p[j];
-                    mqorig = vec_min<J>(p, lane, C.Q, C.L);
+                    for (int j = 0; j < J; ++j) qorig[j] = s.p[j];
+                    mqorig = vec_min_bits<J>(s.p);
                 }
-                const bool masked = P.mask && (HORIZ ? im[(size_t)line * W + pred] : im[(size_t)pred * W + line]) == 0;
-                if (!(masked || mq == 0.f)) {  // :880-881 -- else p stays untouched
-                    partial_opt<J>(p, q, mq, d1, g, lane, C);
+                const bool masked = mask && s.mk == 0;  // :824, :862
+                if (!(masked || mq == 0u)) {            // :880-881 -- else p stays untouched
+                    partial_opt<J>(s.p, q, mq, s.d1, s, sh, rev, lane, C);
                     if (store) {
 #pragma unroll
                         for (int j = 0; j < J; ++j) {
                             const int qq = lane + 64 * j;
-                            if (qq < Q) *reinterpret_cast<f32x4*>(base + (size_t)pos * es + 4 * qq) = p[j];
+                            if (qq < C.Q) *reinterpret_cast<f32x4*>(base + (size_t)pos * es + 4 * qq) = s.p[j];
                         }
                     }
                 }
 #pragma unroll
-                for (int j = 0; j < J; ++j) q[j] = p[j];
-                mq = vec_min<J>(q, lane, C.Q, C.L);
+                for (int j = 0; j < J; ++j) q[j] = s.p[j];
+                mq = vec_min_bits<J>(q);
                 if (wrow) {
-                    const int d = vec_argmin<J>(q, lane, C.Q, C.L, C.minD, mq);
+                    const int d = vec_argmin<J>(q, lane, C.L, C.minD, mq);
                     if (lane == 0) wrow[pos] = d;
                 }
             }

@@ -43,7 +43,12 @@ struct DevParams {
     int max_search_depth;
     int canny_low, canny_high;
     int omp_threads;   // scanline race emulation (0/1 = serial semantics)
+    int gpad, gstride; // colour-difference maps: row stride and left margin (sentinel bytes)
 };
+
+// Left/right margin of the colour-difference maps gv/gh: a scanline step reads 4
+// consecutive bytes at x = line +- (d + minD), d < L, through an aligned 8-byte load.
+__host__ __device__ inline int grad_pad(int maxD) { return ((maxD + 12 + 15) / 16) * 16; }
 
 __device__ __forceinline__ int iabs_(int x) { return x < 0 ? -x : x; }
 __device__ __forceinline__ int ch(uint32_t p, int c) { return (p >> (8 * c)) & 0xff; }
@@ -79,20 +84,21 @@ constexpr int DPP_WAVE_SHL1 = 0x130;    // lane l <- lane l+1
 constexpr int DPP_WAVE_SHR1 = 0x138;    // lane l <- lane l-1
 
 // Wave-wide min of NON-NEGATIVE floats (cost values), result uniform in every lane.
-// Non-negative IEEE floats order like their bit patterns, so the cross-row step runs
-// on the scalar unit as unsigned integer min.
-__device__ __forceinline__ float wave_min_nonneg(float v) {
-    const float inf = __int_as_float(0x7f800000);
-    v = fminf(v, dpp_f<DPP_QUAD_1032>(v, inf));
-    v = fminf(v, dpp_f<DPP_QUAD_2301>(v, inf));
-    v = fminf(v, dpp_f<DPP_ROW_HALF_MIRROR>(v, inf));
-    v = fminf(v, dpp_f<DPP_ROW_MIRROR>(v, inf));
-    uint32_t r0 = __builtin_amdgcn_readlane(__float_as_uint(v), 0);
-    uint32_t r1 = __builtin_amdgcn_readlane(__float_as_uint(v), 16);
-    uint32_t r2 = __builtin_amdgcn_readlane(__float_as_uint(v), 32);
-    uint32_t r3 = __builtin_amdgcn_readlane(__float_as_uint(v), 48);
-    uint32_t m = min(min(r0, r1), min(r2, r3));
-    return __uint_as_float(m);
+// Non-negative IEEE floats order like their bit patterns, so the whole reduction runs
+// as unsigned integer min (DPP within rows, scalar across the four rows): exact, and
+// without the canonicalising v_max the compiler puts in front of every fminf.
+__device__ __forceinline__ float wave_min_nonneg(float x) {
+    uint32_t v = __float_as_uint(x);
+    const uint32_t inf = 0x7f800000u;
+    v = min(v, dpp_u<DPP_QUAD_1032>(v, inf));
+    v = min(v, dpp_u<DPP_QUAD_2301>(v, inf));
+    v = min(v, dpp_u<DPP_ROW_HALF_MIRROR>(v, inf));
+    v = min(v, dpp_u<DPP_ROW_MIRROR>(v, inf));
+    const uint32_t r0 = __builtin_amdgcn_readlane(v, 0);
+    const uint32_t r1 = __builtin_amdgcn_readlane(v, 16);
+    const uint32_t r2 = __builtin_amdgcn_readlane(v, 32);
+    const uint32_t r3 = __builtin_amdgcn_readlane(v, 48);
+    return __uint_as_float(min(min(r0, r1), min(r2, r3)));
 }
 
 // Wave-wide min of u64 keys (e.g. (float_bits << 32) | d for WTA first-min).
