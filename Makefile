@@ -32,6 +32,13 @@ $(LIB): $(OBJS)
 	@mkdir -p $(LIBDIR)
 	$(HIPCC) --offload-arch=$(ARCH) -shared -o $@ $(OBJS)
 
+# experimental variants for on-GPU A/B timing: make exp X=name DEFS="-DTSM_EXP_..."
+exp:
+	@mkdir -p build/exp/$(X)/obj
+	for f in $(HIP_SRCS); do $(HIPCC) $(HIPFLAGS) $(DEFS) -c $(SRC)/$$f.hip -o build/exp/$(X)/obj/$$f.o || exit 1; done
+	for f in $(CPP_SRCS); do $(HIPCC) $(HIPFLAGS) $(DEFS) -c $(SRC)/$$f.cpp -o build/exp/$(X)/obj/$$f.o || exit 1; done
+	$(HIPCC) --offload-arch=$(ARCH) -shared -o build/exp/$(X)/libtsm_adcensus.so build/exp/$(X)/obj/*.o
+
 oracle:
 	$(MAKE) -C oracle
 
@@ -39,4 +46,4 @@ clean:
 	rm -rf build $(LIBDIR)
 	$(MAKE) -C oracle clean
 
-.PHONY: all lib oracle clean
+.PHONY: all lib oracle clean exp

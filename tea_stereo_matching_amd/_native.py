@@ -95,11 +95,12 @@ def load() -> ctypes.CDLL:
     global _lib
     if _lib is not None:
         return _lib
-    if not os.path.exists(LIB_PATH):
+    path = os.environ.get("TSM_LIB", LIB_PATH)  # developer hook: an experimental build
+    if not os.path.exists(path):
         raise ImportError(
-            f"{LIB_PATH} not found: build the gfx950 library first "
+            f"{path} not found: build the gfx950 library first "
             "(`make lib` or `python -c 'import __graft_entry__ as g; g.build()'`)")
-    lib = ctypes.CDLL(LIB_PATH)
+    lib = ctypes.CDLL(path)
     for name, (res, args) in SIGNATURES.items():
         fn = getattr(lib, name)
         fn.restype = res

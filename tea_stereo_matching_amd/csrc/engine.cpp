@@ -94,9 +94,11 @@ struct Workspace {
     uint32_t* img_orig = nullptr;  // [2][H][W] packed BGR
     uint32_t* img = nullptr;       // [2][H][W] matched images (== img_orig for RGB)
     uint32_t* img_tmp = nullptr;   // HSI scratch
-    uint32_t* desc = nullptr;      // [2][H][W][12]
+    uint32_t* desc = nullptr;      // [2][H][W][16]
     float* vol = nullptr;          // [2][H][W][Lp]
     uint32_t* arms = nullptr;      // [2][H][W]
+    uint32_t* cost_ctr = nullptr;  // cost-walk unit counter (never reset, see k_cost.hip)
+    uint32_t cost_ctr_base = 0;
     int32_t* ws = nullptr;         // [2][2][H][W]
     uint8_t* gv = nullptr;         // [2][H][gstride] (sentinel margins)
     uint8_t* gh = nullptr;         // [2][H][gstride]
@@ -168,9 +170,9 @@ size_t workspace_bytes(int H, int W, int L) {
     const size_t N = (size_t)H * W, Lp = (size_t)round_up4(L);
     size_t b = 0;
     b += 3 * 2 * N * 4;        // img_orig, img, img_tmp
-    b += 2 * N * 12 * 4;       // desc
+    b += 2 * N * 16 * 4;       // desc
     b += 2 * N * Lp * 4;       // vol
-    b += 2 * N * 4;            // arms
+    b += 2 * N * 4 + 256;      // arms, cost-walk counter
     b += 4 * N * 4;            // ws
     b += 4 * (size_t)H * (W + 2 * grad_pad(L) + 16);  // gv, gh (upper bound)
     b += N * (4 * 8 + 2 * 20 + 1 * 6 + 2 * 2 + 4); // refine maps
@@ -272,9 +274,10 @@ int ensure_workspace(tsm_adc* h, Workspace* w, int H, int W) {
     } else {
         w->img = w->img_orig;
     }
-    A(w->desc, 2 * N * 12 * 4);
+    A(w->desc, 2 * N * 16 * 4);
     A(w->vol, 2 * N * (size_t)Lp * 4);
     A(w->arms, 2 * N * 4);
+    A(w->cost_ctr, 256);
     A(w->ws, 4 * N * 4);
     {
         const int gp = grad_pad(h->max_disparity);
@@ -317,6 +320,8 @@ int ensure_workspace(tsm_adc* h, Workspace* w, int H, int W) {
     HIP_OK(hipMemcpy(w->lutB, lb.data(), lb.size() * 4, hipMemcpyHostToDevice));
     // padded lanes of the volume are never read as labels; keep them defined anyway
     HIP_OK(hipMemset(w->vol, 0, 2 * N * (size_t)Lp * 4));
+    HIP_OK(hipMemset(w->cost_ctr, 0, 256));
+    w->cost_ctr_base = 0;
     w->H = H;
     w->W = W;
     w->L = L;
@@ -414,7 +419,8 @@ int run_pipeline(tsm_adc* h, Workspace* w, const uint8_t* d_left, const uint8_t*
     launch_census(w->img, w->desc, P, st);
     mark();
     // --- cost volume -------------------------------------------------------------
-    if (launch_cost_volume(w->img, w->desc, w->lutA, w->lutA_n, w->lutB, w->vol, P, st) != 0)
+    if (launch_cost_volume(w->img, w->desc, w->lutA, w->lutA_n, w->lutB, w->vol, P, w->cost_ctr,
+                           w->cost_ctr_base, st) != 0)
         return fail(h, TSM_ERR_UNSUPPORTED, "cost volume: label count");
     mark();
     if (dump && dump->images) {

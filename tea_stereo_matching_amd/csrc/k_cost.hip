@@ -12,6 +12,9 @@
 // The AD-Census cost 2 - exp(-ad/lambdaAD) - exp(-census/lambdaCensus) (:518) is
 // evaluated through two host-built tables (glibc expf on the exact arguments the
 // reference feeds to std::exp), so the device result is bit-identical.
+#include <algorithm>
+#include <stdlib.h>
+
 #include "tsm_device.h"
 #include "tsm_launch.h"
 
@@ -102,10 +105,13 @@ __global__ void k_gauss_median(const uint32_t* __restrict__ src, uint32_t* __res
 }
 
 // ---------------------------------------------------------------------------
-// census descriptors: desc[v][y][x][12]
+// census descriptors: desc[v][y][x][16]
 //   RGB: words 0..5 = gt planes (ch0 lo,hi, ch1 lo,hi, ch2 lo,hi), 6..11 = lt planes
 //   HSI: words 0..1 = hue "positive" plane, 2..5 = sat/int gt, 6..9 = sat/int lt
-// Border pixels (window leaving the image) never reach the cost (:562-566): zeros.
+//   word 12 = the pixel's packed colour (AD term, mask tests), words 13..15 = 0.
+// One 64-B record per pixel, so the cost walk fetches a whole record with one scalar
+// load.  Border pixels (window leaving the image) never reach the cost (:562-566):
+// their planes are zero.
 // ---------------------------------------------------------------------------
 template <int CW, int CHh, bool HSI>
 __global__ void k_census_desc(const uint32_t* __restrict__ img, uint32_t* __restrict__ desc,
@@ -121,8 +127,8 @@ __global__ void k_census_desc(const uint32_t* __restrict__ img, uint32_t* __rest
 #pragma unroll
     for (int k = 0; k < 12; ++k) w[k] = 0;
     const uint32_t* im = img + (size_t)v * H * W;
+    const uint32_t c = im[(size_t)y * W + x];
     if (x - hw >= 0 && x + hw < W && y - hh >= 0 && y + hh < H) {
-        const uint32_t c = im[(size_t)y * W + x];
         const int c0 = ch(c, 0), c1 = ch(c, 1), c2 = ch(c, 2);
         // fully unrolled: bit position and word index are compile-time constants
 #pragma unroll
@@ -154,152 +160,307 @@ __global__ void k_census_desc(const uint32_t* __restrict__ img, uint32_t* __rest
             }
         }
     }
-    uint4* o = reinterpret_cast<uint4*>(desc + (((size_t)v * H + y) * W + x) * 12);
-    o[0] = make_uint4(w[0], w[1], w[2], w[3]);
-    o[1] = make_uint4(w[4], w[5], w[6], w[7]);
-    o[2] = make_uint4(w[8], w[9], w[10], w[11]);
+    u32x4* o = reinterpret_cast<u32x4*>(desc + (((size_t)v * H + y) * W + x) * 16);
+    o[0] = u32x4{w[0], w[1], w[2], w[3]};
+    o[1] = u32x4{w[4], w[5], w[6], w[7]};
+    o[2] = u32x4{w[8], w[9], w[10], w[11]};
+    o[3] = u32x4{c, 0u, 0u, 0u};
 }
 
 // ---------------------------------------------------------------------------
-// cost-volume build
+// cost-volume build: one wave walks a row segment, the matched-against records held
+// in a lane-shift register
 // ---------------------------------------------------------------------------
-// One workgroup = one image row segment of CT pixels of one view.  The descriptors
-// and colours of the segment's fixed side (CT pixels) and varying side (CT + L - 1
-// pixels) are staged in LDS structure-of-arrays; each wave walks CT/4 pixels, lanes
-// own disparities d = lane + 64*e, so every LDS read of the varying side is 64
-// consecutive dwords (conflict-free) and every store is 256 contiguous bytes of the
-// pixel's L-vector.
-constexpr int CT = 64;          // pixels per workgroup
-constexpr int CT_THREADS = 256; // 4 waves
+// Lanes own E consecutive labels k = E*lane + e (E = 4 up to 256 labels, 8 up to 512), so
+// a pixel's L-vector leaves as E/4 16-B stores per lane (784 contiguous bytes at L = 193).  View 0 pairs the fixed pixel
+// left(j - minD) with right(j - k) at label k; view 1 pairs right(j + minD) with
+// left(j + k) (costInitialize :542-579).  View 0 walks j upward and view 1 walks it
+// downward, so in BOTH views the next pixel needs at label k the record that label k-1
+// holds now: the label axis moves up one slot per step.  Inside a lane that is a
+// rotation of the E slot registers (compile-time renaming, no data movement); one DPP
+// wave_shr:1 per word carries the top slot into the next lane, and the one record that enters
+// (label 0: varying column j) arrives by a wave-uniform scalar load and is written into
+// lane 0.  The fixed pixel's record is wave-uniform as well (SGPR operands).  A cost
+// cell is 6 x (and, and_or, bcnt) + one v_sad_u8 + two LDS table reads; no descriptor
+// ever goes through LDS.  Census and AD are symmetric in (left, right), so both views
+// run the same arithmetic.
+constexpr int CW_THREADS = 256;   // 4 independent waves per workgroup (tables shared)
+constexpr int CW_LUTB = 192;      // lutB slot (188 used); padding entries follow it
+constexpr int CW_CHUNK = 16;      // staging granule: 16 records x 64 B = one LDS-DMA per wave
+constexpr int CW_SEG = 48;        // pixels per walk unit
 
-template <int E, bool HSI>
-__global__ __launch_bounds__(CT_THREADS) void k_cost_volume(
-    const uint32_t* __restrict__ img, const uint32_t* __restrict__ desc,
-    const float* __restrict__ lutA, int lutA_n, const float* __restrict__ lutB,
-    float* __restrict__ vol, DevParams Pk) {
+template <int N>
+struct IC { static constexpr int value = N; };
+
+// staged records per stream: steps run in whole groups of E and read one record ahead
+__host__ __device__ inline int cost_stage_slots(int seg_len, int E) {
+    return (seg_len + E + 1 + CW_CHUNK - 1) / CW_CHUNK * CW_CHUNK;
+}
+
+// popcount accumulated in one instruction; opaque to the optimiser, which otherwise
+// re-associates the census sum into add3 trees and distributes the table-address
+// scaling over every term
+__device__ __forceinline__ uint32_t bcnt_acc(uint32_t x, uint32_t acc) {
+    uint32_t r;
+    asm("v_bcnt_u32_b32 %0, %1, %2" : "=v"(r) : "v"(x), "v"(acc));
+    return r;
+}
+
+#ifdef TSM_EXP_STAMPS
+// experiment build only: per-wave phase timestamps (s_memtime) for timeline analysis
+__device__ unsigned long long g_stamps[65536 * 8];
+#define CW_STAMP(i)                                                                   \
+    do {                                                                              \
+        if (lane == 0 && gw < 65536) g_stamps[(size_t)gw * 8 + (i)] = __builtin_amdgcn_s_memtime(); \
+    } while (0)
+#else
+#define CW_STAMP(i) do { } while (0)
+#endif
+
+template <int E, bool HSI, bool MASK>
+__global__ __launch_bounds__(CW_THREADS) void k_cost_walk(
+    const uint32_t* __restrict__ desc, const float* __restrict__ lutA, int lutA_n,
+    const float* __restrict__ lutB, float* __restrict__ vol, DevParams Pk, int seg_len, int nseg,
+    uint32_t* __restrict__ ctr, uint32_t ctr_base) {
     const DevParams P = Pk;  // kernel args -> registers once (no per-use kernarg reloads)
-    extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
+    // tables at fixed LDS addresses (table reads take the base as an immediate offset):
+    //   sB[0..187] census term, sB[192..383] = -inf: padding labels (k >= L) start their
+    //   census sum at 192, so 2 - A - (-inf) = +inf with no per-label select
+    __shared__ __attribute__((aligned(16))) float s_lut[2 * CW_LUTB + (HSI ? 2816 : 768)];
+    extern __shared__ __attribute__((aligned(16))) u32x4 smem_stage[];
+    float* sB = s_lut;
+    float* sA = s_lut + 2 * CW_LUTB;
     const int H = P.H, W = P.W, L = P.L, Lp = P.Lp;
-    const int v = blockIdx.z;
-    const int y = blockIdx.y;
-    const int j0 = blockIdx.x * CT;
-    const int NV = CT + L - 1; // varying-side span
-    // LDS carve: lutA | lutB(188) | Fdesc[12][CT] | Fcol[CT] | Vdesc[12][NV] | Vcol[NV]
-    float* sA = reinterpret_cast<float*>(smem);
-    float* sB = sA + lutA_n;
-    uint32_t* sF = reinterpret_cast<uint32_t*>(sB + 188);
-    uint32_t* sFc = sF + 12 * CT;
-    uint32_t* sV = sFc + CT;
-    uint32_t* sVc = sV + 12 * NV;
-
-    for (int i = threadIdx.x; i < lutA_n; i += CT_THREADS) sA[i] = lutA[i];
-    for (int i = threadIdx.x; i < 188; i += CT_THREADS) sB[i] = lutB[i];
-
-    // view 0: fixed = left  at colL = j - minD, varying = right at colR = j - d
-    // view 1: fixed = right at colR = j + minD, varying = left  at colL = j + d
-    const int fimg = v == 0 ? 0 : 1;
-    const int vimg = 1 - fimg;
-    const int foff = v == 0 ? -P.minD : P.minD;
-    const int vbase = v == 0 ? j0 - (L - 1) : j0; // x of varying slot 0
-    const uint32_t* dF = desc + (size_t)fimg * H * W * 12 + (size_t)y * W * 12;
-    const uint32_t* dV = desc + (size_t)vimg * H * W * 12 + (size_t)y * W * 12;
-    const uint32_t* iF = img + (size_t)fimg * H * W + (size_t)y * W;
-    const uint32_t* iV = img + (size_t)vimg * H * W + (size_t)y * W;
-    // coalesced staging: consecutive threads read consecutive descriptor words
-    for (int t = threadIdx.x; t < CT * 12; t += CT_THREADS) {
-        const int s = t / 12, k = t - 12 * (t / 12);
-        const int x = j0 + s + foff;
-        sF[k * CT + s] = (x >= 0 && x < W) ? dF[(size_t)x * 12 + k] : 0u;
-    }
-    for (int s = threadIdx.x; s < CT; s += CT_THREADS) {
-        const int x = j0 + s + foff;
-        sFc[s] = (x >= 0 && x < W) ? iF[x] : 0u;
-    }
-    for (int t = threadIdx.x; t < NV * 12; t += CT_THREADS) {
-        const int s = t / 12, k = t - 12 * (t / 12);
-        const int x = vbase + s;
-        sV[k * NV + s] = (x >= 0 && x < W) ? dV[(size_t)x * 12 + k] : 0u;
-    }
-    for (int s = threadIdx.x; s < NV; s += CT_THREADS) {
-        const int x = vbase + s;
-        sVc[s] = (x >= 0 && x < W) ? iV[x] : 0u;
-    }
-    __syncthreads();
-
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int lane = threadIdx.x & 63;
-    const int hw = P.censusW / 2, hh = P.censusH / 2;
+    (void)ctr;
+    (void)ctr_base;
+    // one walk unit (view, row, segment) per wave; the unit's loads (ring prologue and
+    // warm-up gather) are issued before the table fill's barrier so their latencies overlap
+    const int gw0 = blockIdx.x * (CW_THREADS / 64) + wave;
+    const bool active = gw0 < 2 * H * nseg;
+    const int gw = active ? gw0 : 0;
+    CW_STAMP(0);
+#ifdef TSM_EXP_STAMPS
+    if (lane == 0 && gw < 65536) {
+        unsigned hw_id, xcc;
+        asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hw_id));
+        asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
+        g_stamps[(size_t)gw * 8 + 5] = hw_id | ((unsigned long long)xcc << 32);
+    }
+#endif
+    const int seg = gw % nseg;
+    const int row = gw / nseg;
+    const int v = row / H, y = row - v * H;
+    const int foff = v == 0 ? -P.minD : P.minD;
+    const int x_lo = seg * seg_len;
+    const int count = min(seg_len, W - x_lo);
+    const int j0 = x_lo;  // both views walk j upward: stores stream forward through HBM
+    const int vtop = E * 64 - 1;  // view 1 feeds its shift register at the top label
+    const int hw = P.censusW >> 1, hh = P.censusH >> 1;
     const bool rowOut = y - hh < 0 || y + hh >= H;
+    constexpr int NW = HSI ? 11 : 13;  // shifted words: descriptor planes + colour
+    constexpr int CWORD = 12;          // colour word of a record
     const uint32_t vmask_hi = (P.censusW * P.censusH - 1) >= 64
                                   ? 0xffffffffu
                                   : ((1u << ((P.censusW * P.censusH - 1) - 32)) - 1u);
-    for (int s = wave; s < CT; s += 4) {
-        const int j = j0 + s;
-        if (j >= W) break;
-        float* out = vol + (((size_t)v * H + y) * W + j) * Lp;
-        const uint32_t fcol = sFc[s];
-        // mask mode: the pixel of this view black -> 2.f for every d (:551-555)
-        const uint32_t own = img[((size_t)v * H + y) * W + j];
-        const bool ownBlack = P.mask && own == 0;
-        uint32_t f[12];
+    const uint32_t* dF = desc + ((size_t)v * H + y) * W * 16;        // fixed image
+    const uint32_t* dV = desc + ((size_t)(1 - v) * H + y) * W * 16;  // varying image
+    float* orow = vol + ((size_t)v * H + y) * W * Lp + E * lane;
+    auto clampx = [&](int x) { return x < 0 ? 0 : (x >= W ? W - 1 : x); };
+
+    // The unit's two wave-uniform record streams (fixed records x = j + foff, entering
+    // records x = j (view 0) or j + vtop (view 1)) are staged in LDS up front by LDS-DMA
+    // (global_load_lds_dwordx4: lane i's 16 bytes land at chunk base + 16 i, i.e. record
+    // i/4, quarter i%4; no staging registers): per step they are broadcast LDS reads,
+    // never an L2/HBM round trip.
+    const int slots = cost_stage_slots(seg_len, E);
+    u32x4* stF = smem_stage + (size_t)wave * 2 * slots * 4;
+    u32x4* stE = stF + (size_t)slots * 4;
+    const int rq = lane & 3, rr = lane >> 2;  // this lane's quarter / record of a chunk
+    auto dma_chunk = [&](int t0) {  // records t0 .. t0+CW_CHUNK-1 (t0 a multiple of CW_CHUNK)
+        const int t = t0 + rr;
+        const int base = t0 * 4;
+        __builtin_amdgcn_global_load_lds(
+            reinterpret_cast<const u32x4*>(dF + (size_t)clampx(j0 + t + foff) * 16) + rq, stF + base, 16, 0, 0);
+        __builtin_amdgcn_global_load_lds(
+            reinterpret_cast<const u32x4*>(dV + (size_t)clampx(j0 + t + (v == 0 ? 0 : vtop)) * 16) + rq,
+            stE + base, 16, 0, 0);
+    };
+    for (int c = 0; c < slots; c += CW_CHUNK) dma_chunk(c);
+
+    for (int i = threadIdx.x; i < lutA_n; i += CW_THREADS) sA[i] = lutA[i];
+    for (int i = threadIdx.x; i < 2 * CW_LUTB; i += CW_THREADS)
+        sB[i] = i < 188 ? lutB[i] : (i >= CW_LUTB ? -__int_as_float(0x7f800000) : 0.f);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // ring prologue landed (LDS-DMA)
+    __syncthreads();  // tables ready: the kernel's only barrier
+    if (!active) return;
+    CW_STAMP(1);
+
+    // warm-up: label k = E*lane + e holds the varying record at x = j0 - k (view 0) or
+    // j0 + k (view 1), clamped: labels whose column leaves the image are border cells,
+    // fixed up per step.  (Rotation 0: label offset e sits in slot e in both views.)
+    uint32_t V[NW][E];
 #pragma unroll
-        for (int k = 0; k < 12; ++k) f[k] = sF[k * CT + s];
-        const int colF = j + foff;
+    for (int e = 0; e < E; ++e) {
+        int x = v == 0 ? j0 - (E * lane + e) : j0 + (E * lane + e);
+        x = x < 0 ? 0 : (x >= W ? W - 1 : x);
+        const u32x4* r = reinterpret_cast<const u32x4*>(dV + (size_t)x * 16);
+        const u32x4 a = r[0], b = r[1], c = r[2], d = r[3];
+        const uint32_t rec[13] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w, c.x, c.y, c.z, c.w, d.x};
+#pragma unroll
+        for (int w = 0; w < NW; ++w) V[w][e] = rec[w < NW - 1 ? w : CWORD];
+    }
+
+
+    // record -> NW shifted words (descriptor planes, then the colour)
+    auto pick = [&](const u32x4& a, const u32x4& b, const u32x4& c, const u32x4& d, uint32_t (&o)[NW]) {
+        const uint32_t rec[13] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w, c.x, c.y, c.z, c.w, d.x};
+#pragma unroll
+        for (int w = 0; w < NW; ++w) o[w] = rec[w < NW - 1 ? w : CWORD];
+    };
+    auto load_staged = [&](const u32x4* st, int t, uint32_t (&o)[NW]) {
+        const int i = t * 4;
+        const uint32_t* r1 = reinterpret_cast<const uint32_t*>(st + i);
+        pick(st[i + 0], st[i + 1], st[i + 2], u32x4{r1[CWORD], 0u, 0u, 0u}, o);
+    };
+
+    // View 0 pairs label k with right(j - k): the next pixel's label k is this pixel's
+    // label k-1, so the label axis moves UP one slot per step (slot of offset e at
+    // rotation R: (e - R) mod E; DPP wave_shr carries lanes up, lane 0 takes the entering
+    // record x = j).  View 1 pairs label k with left(j + k): the label axis moves DOWN
+    // (slot (e + R) mod E; wave_shl, lane 63 takes x = j + vtop).
+    auto walk = [&](auto UPc) {
+    constexpr bool UP = decltype(UPc)::value == 0;
+    const float kInf = __int_as_float(0x7f800000);
+    uint32_t padoff[E];  // census start: 0, or CW_LUTB for padding labels (+inf cost)
+#pragma unroll
+    for (int e = 0; e < E; ++e) padoff[e] = (!MASK && E * lane + e >= L) ? CW_LUTB : 0u;
+    // fixed records double-buffered by step parity (compile-time), no register copies
+    uint32_t FA[NW], FB[NW], En[NW];
+    load_staged(stF, 0, FA);
+
+    // one step at rotation R
+    auto step = [&](auto Rc, bool fast, int t) {  // fast: interior group, no border tests
+        constexpr int R = decltype(Rc)::value;
+        uint32_t(&F)[NW] = (R & 1) ? FB : FA;
+        uint32_t(&Fn)[NW] = (R & 1) ? FA : FB;
+        const int j = j0 + t;
+        // the next step's records (steps past the segment end run on clamped records
+        // and store nothing: no branches)
+        load_staged(stF, t + 1, Fn);
+        load_staged(stE, t + 1, En);
+        // census of the E cells, interleaved word by word (E independent bcnt chains)
+        uint32_t cen[E];
+#pragma unroll
+        for (int e = 0; e < E; ++e) cen[e] = padoff[e];
+        if (!HSI) {
+#pragma unroll
+            for (int k = 0; k < 6; ++k)
+#pragma unroll
+                for (int e = 0; e < E; ++e) {
+                    const int s = UP ? (e - R + E) % E : (e + R) % E;
+                    cen[e] = bcnt_acc((F[k] & V[6 + k][s]) | (F[6 + k] & V[k][s]), cen[e]);
+                }
+        } else {
+#pragma unroll
+            for (int e = 0; e < E; ++e) {
+                const int s = UP ? (e - R + E) % E : (e + R) % E;
+                cen[e] = padoff[e] + __builtin_popcount(~(F[0] & V[0][s])) +
+                         __builtin_popcount(~(F[1] & V[1][s]) & vmask_hi);
+#pragma unroll
+                for (int k = 2; k < 6; ++k)
+                    cen[e] += __builtin_popcount((F[k] & V[4 + k][s]) | (F[4 + k] & V[k][s]));
+            }
+        }
+        float c[E];
 #pragma unroll
         for (int e = 0; e < E; ++e) {
-            const int d = lane + 64 * e;
-            if (d >= Lp) break;
-            float c;
-            if (d >= L) {
-                c = __int_as_float(0x7f800000);
+            const int s = UP ? (e - R + E) % E : (e + R) % E;
+            const uint32_t vc = V[NW - 1][s], fc = F[NW - 1];
+            int ai;
+            if (!HSI) {
+                ai = (int)__builtin_amdgcn_sad_u8(fc, vc, 0u);
             } else {
-                const int colV = v == 0 ? j - d : j + d;
-                const int colL = v == 0 ? colF : colV;
-                const int colR = v == 0 ? colV : colF;
-                const bool out_ = rowOut || colL - hw < 0 || colL + hw >= W || colR - hw < 0 ||
-                                  colR + hw >= W;
-                if (ownBlack || out_) {
-                    c = 2.f;
-                } else {
-                    const int sv = v == 0 ? (L - 1 - d) + s : s + d; // colV - vbase
-                    uint32_t vd[12];
-#pragma unroll
-                    for (int k = 0; k < 12; ++k) vd[k] = sV[k * NV + sv];
-                    const uint32_t vcol = sVc[sv];
-                    // (left, right) roles
-                    const uint32_t* dl = v == 0 ? f : vd;
-                    const uint32_t* dr = v == 0 ? vd : f;
-                    const uint32_t cl = v == 0 ? fcol : vcol;
-                    const uint32_t cr = v == 0 ? vcol : fcol;
-                    int cen;
-                    if (!HSI) {
-                        cen = 0;
-#pragma unroll
-                        for (int k = 0; k < 6; ++k)
-                            cen += __popc((dl[k] & dr[6 + k]) | (dl[6 + k] & dr[k]));
-                    } else {
-                        cen = __popc(~(dl[0] & dr[0])) + __popc(~(dl[1] & dr[1]) & vmask_hi);
-#pragma unroll
-                        for (int k = 2; k < 6; ++k)
-                            cen += __popc((dl[k] & dr[4 + k]) | (dl[4 + k] & dr[k]));
-                    }
-                    int ai;
-                    if (!HSI) {
-                        ai = iabs_(ch(cl, 0) - ch(cr, 0)) + iabs_(ch(cl, 1) - ch(cr, 1)) +
-                             iabs_(ch(cl, 2) - ch(cr, 2));
-                    } else {
-                        const int hd = iabs_(ch(cl, 0) - ch(cr, 0));
-                        ai = 2 * min(hd, 255 - hd) +
-                             5 * (iabs_(ch(cl, 1) - ch(cr, 1)) + iabs_(ch(cl, 2) - ch(cr, 2)));
-                    }
-                    // mask mode: black centre on either side -> census = +inf (:459-460)
-                    if (P.mask && (cl == 0 || cr == 0)) cen = 187;
-                    c = 2.f - sA[ai] - sB[cen];
-                }
+                const int hd = (int)__builtin_amdgcn_sad_u8(fc & 0xffu, vc & 0xffu, 0u);
+                ai = 2 * min(hd, 255 - hd) +
+                     5 * (int)__builtin_amdgcn_sad_u8(fc & 0xffff00u, vc & 0xffff00u, 0u);
             }
-            out[d] = c;
+            // mask mode: black centre on either side -> census = +inf (:459-460)
+            if (MASK && (fc == 0 || vc == 0)) cen[e] = 187;
+#ifdef TSM_EXP_NOLUT
+            c[e] = (float)ai - (float)cen[e];
+#else
+            c[e] = 2.f - sA[ai] - sB[cen[e]];
+#endif
+        }
+        // border cells (either 9x7 window leaves the image, :562-566) and masked own
+        // pixels (:551-555) cost 2; wave-uniform test first, per-label only near borders
+        if (!fast) {
+        const int xf = j + foff;
+        bool fixed_ok = !rowOut && xf - hw >= 0 && xf + hw < W;
+        if (MASK) fixed_ok = fixed_ok && dF[(size_t)__builtin_amdgcn_readfirstlane(j) * 16 + CWORD] != 0u;
+        const int klo = v == 0 ? j - (W - 1 - hw) : hw - j;
+        const int khi = v == 0 ? j - hw : W - 1 - hw - j;
+        if (!(fixed_ok && klo <= 0 && khi >= L - 1)) {
+#pragma unroll
+            for (int e = 0; e < E; ++e) {
+                const int k = E * lane + e;
+                c[e] = (fixed_ok && k >= klo && k <= khi) || k >= L ? c[e] : 2.f;
+            }
+        }
+        }
+        if (MASK) {  // mask mode overrides census indices: padding needs its own select
+#pragma unroll
+            for (int e = 1; e < E; ++e) c[e] = E * lane + e >= L ? kInf : c[e];
+        }
+#ifdef TSM_EXP_NOSTORE
+        if ((fast || t < count) && c[0] == -12345.f) {
+#else
+        if (fast || t < count) {
+#endif
+#pragma unroll
+            for (int q = 0; q < E / 4; ++q)
+                if (E * lane + 4 * q < Lp)
+                    *reinterpret_cast<f32x4*>(orow + (size_t)j * Lp + 4 * q) =
+                        f32x4{c[4 * q], c[4 * q + 1], c[4 * q + 2], c[4 * q + 3]};
+        }
+        // advance: view 0: the slot of offset E-1 becomes offset 0 of the next rotation,
+        // fed from lane-1 (lane 0 has no source and keeps `old`, the entering word);
+        // view 1: the slot of offset 0 becomes offset E-1, fed from lane+1 (lane 63 keeps
+        // the entering word)
+        constexpr int s3 = UP ? (2 * E - 1 - R) % E : R % E;
+#pragma unroll
+        for (int w = 0; w < NW; ++w)
+            V[w][s3] = (uint32_t)__builtin_amdgcn_update_dpp((int)En[w], (int)V[w][s3],
+                                                             UP ? DPP_WAVE_SHR1 : DPP_WAVE_SHL1,
+                                                             0xF, 0xF, false);
+    };
+    // interior steps (every label's windows inside the image) form one run of t: the
+    // walk takes a branch-free body for whole groups of E steps inside it
+    const int jlo = max(v == 0 ? hw + L - 1 : hw, hw - foff);
+    const int jhi = min(v == 0 ? W - 1 - hw : W - hw - L, W - 1 - hw - foff);
+    const int tf_lo = jlo - j0;
+    const int tf_hi = min(jhi - j0, count - 1);
+    const bool rows_ok = !MASK && !rowOut;
+    CW_STAMP(2);
+    for (int t = 0; t < count; t += E) {
+        const bool fast = rows_ok && t >= tf_lo && t + E - 1 <= tf_hi;
+        step(IC<0>{}, fast, t);
+        step(IC<1>{}, fast, t + 1);
+        step(IC<2>{}, fast, t + 2);
+        step(IC<3>{}, fast, t + 3);
+        if constexpr (E == 8) {
+            step(IC<4>{}, fast, t + 4);
+            step(IC<5>{}, fast, t + 5);
+            step(IC<6>{}, fast, t + 6);
+            step(IC<7>{}, fast, t + 7);
         }
     }
+    };
+    if (v == 0) walk(IC<0>{});
+    else walk(IC<1>{});
+    CW_STAMP(3);
 }
 
 // ---------------------------------------------------------------------------
@@ -336,34 +497,66 @@ void launch_census(const uint32_t* img, uint32_t* desc, const DevParams& P, hipS
     trace_point("k_census_desc", st);
 }
 
-size_t cost_volume_lds_bytes(const DevParams& P, int lutA_n) {
-    const int NV = CT + P.L - 1;
-    return sizeof(float) * (size_t)(lutA_n + 188) + sizeof(uint32_t) * (size_t)(13 * CT + 13 * NV);
+// Walk unit length: each unit pays a 256-record warm-up gather, so units are long
+// enough to amortise it and short enough that the pull queue balances the SIMDs.
+static int cost_seg_len(const DevParams& P) {
+    static const int env = [] {
+        const char* e = getenv("TSM_COST_SEG");  // tuning override
+        return e ? atoi(e) : 0;
+    }();
+    if (env >= 8) return (env + 7) / 8 * 8;
+    (void)P;
+    return CW_SEG;
 }
 
-template <int E, bool HSI>
-static void launch_cost_t(const uint32_t* img, const uint32_t* desc, const float* lutA, int lutA_n,
-                          const float* lutB, float* vol, const DevParams& P, hipStream_t st) {
-    dim3 g((P.W + CT - 1) / CT, P.H, 2);
-    const size_t lds = cost_volume_lds_bytes(P, lutA_n);
-    hipLaunchKernelGGL((k_cost_volume<E, HSI>), g, dim3(CT_THREADS), lds, st, img, desc, lutA,
-                       lutA_n, lutB, vol, P); trace_point("k_cost_volume<E", st);
+size_t cost_volume_lds_bytes(const DevParams& P, int lutA_n) {
+    (void)P;
+    (void)lutA_n;  // the tables are static LDS; this is the dynamic ring part
+    const int E = P.Lp <= 256 ? 4 : 8;
+    return (size_t)(CW_THREADS / 64) * 2 * cost_stage_slots(cost_seg_len(P), E) * 64;
+}
+
+template <int E, bool HSI, bool MASK>
+static void launch_cost_t(const uint32_t* desc, const float* lutA, int lutA_n, const float* lutB,
+                          float* vol, const DevParams& P, uint32_t* ctr, uint32_t& ctr_base,
+                          hipStream_t st) {
+    const int seg_len = cost_seg_len(P);
+    const int nseg = (P.W + seg_len - 1) / seg_len;
+    const int units = 2 * P.H * nseg;
+    const int waves = units;
+    const int wpb = CW_THREADS / 64;
+    dim3 g((waves + wpb - 1) / wpb);
+    hipLaunchKernelGGL((k_cost_walk<E, HSI, MASK>), g, dim3(CW_THREADS), cost_volume_lds_bytes(P, lutA_n), st,
+                       desc, lutA, lutA_n, lutB, vol, P, seg_len, nseg, ctr, ctr_base);
+    trace_point("k_cost_walk", st);
+    ctr_base += (uint32_t)units + (uint32_t)(g.x * wpb);  // every wave overshoots once
 }
 
 int launch_cost_volume(const uint32_t* img, const uint32_t* desc, const float* lutA, int lutA_n,
-                       const float* lutB, float* vol, const DevParams& P, hipStream_t st) {
-    const int E = (P.Lp + 63) / 64;
+                       const float* lutB, float* vol, const DevParams& P, uint32_t* ctr,
+                       uint32_t& ctr_base, hipStream_t st) {
+    (void)img;
     const bool hsi = P.color_model == 1;
-#define CASE(e)                                                                          \
-    case e:                                                                              \
-        if (hsi) launch_cost_t<e, true>(img, desc, lutA, lutA_n, lutB, vol, P, st);      \
-        else launch_cost_t<e, false>(img, desc, lutA, lutA_n, lutB, vol, P, st);         \
-        return 0;
-    switch (E) {
-        CASE(1) CASE(2) CASE(3) CASE(4) CASE(5) CASE(6) CASE(7) CASE(8)
-        default: return -1;
+#define CASE(E)                                                                                    \
+    if (hsi) {                                                                                     \
+        if (P.mask) launch_cost_t<E, true, true>(desc, lutA, lutA_n, lutB, vol, P, ctr, ctr_base, st);  \
+        else launch_cost_t<E, true, false>(desc, lutA, lutA_n, lutB, vol, P, ctr, ctr_base, st);        \
+    } else {                                                                                       \
+        if (P.mask) launch_cost_t<E, false, true>(desc, lutA, lutA_n, lutB, vol, P, ctr, ctr_base, st); \
+        else launch_cost_t<E, false, false>(desc, lutA, lutA_n, lutB, vol, P, ctr, ctr_base, st);       \
     }
+    // one wave holds the whole label axis: E labels per lane
+    if (P.Lp <= 256) { CASE(4) }
+    else if (P.Lp <= 512) { CASE(8) }
+    else return -1;
 #undef CASE
+    return 0;
 }
 
 }  // namespace tsm
+
+#ifdef TSM_EXP_STAMPS
+extern "C" int tsm_exp_stamps(void* host, size_t bytes) {
+    return (int)hipMemcpyFromSymbol(host, HIP_SYMBOL(tsm::g_stamps), bytes, 0, hipMemcpyDeviceToHost);
+}
+#endif

@@ -2,7 +2,7 @@
 //
 // HBM layout of one pair's workspace (see DESIGN.md "Data layout"):
 //   img   [2][H][W]      u32  packed B|G<<8|R<<16 of the matched view images
-//   desc  [2][H][W][12]  u32  ternary census descriptors (gt/lt bit planes)
+//   desc  [2][H][W][16]  u32  ternary census records (gt/lt bit planes + colour)
 //   vol   [2][H][W][Lp]  f32  pixel-major cost volume, Lp = round_up(L, 4)
 //   arms  [2][H][W]      u32  packed u8 arms: up | down<<8 | left<<16 | right<<24
 //   ws    [2][2][H][W]   i32  cross-window sizes (horizontal-first, vertical-first)

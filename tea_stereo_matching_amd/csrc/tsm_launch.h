@@ -19,8 +19,11 @@ void launch_hsi(const uint32_t* src, uint32_t* tmp, uint32_t* dst, int H, int W,
                 hipStream_t st);
 void launch_census(const uint32_t* img, uint32_t* desc, const DevParams& P, hipStream_t st);
 size_t cost_volume_lds_bytes(const DevParams& P, int lutA_n);
+// ctr: a device word owned by the workspace; ctr_base: its host-side launch offset,
+// advanced by the call (the counter is never reset between launches)
 int launch_cost_volume(const uint32_t* img, const uint32_t* desc, const float* lutA, int lutA_n,
-                       const float* lutB, float* vol, const DevParams& P, hipStream_t st);
+                       const float* lutB, float* vol, const DevParams& P, uint32_t* ctr,
+                       uint32_t& ctr_base, hipStream_t st);
 
 // k_aggregate.hip
 void launch_arms(const uint32_t* img, uint32_t* arms, const DevParams& P, hipStream_t st);

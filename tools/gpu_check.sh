@@ -27,6 +27,11 @@ for s in "$@"; do
               step prof 600 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof -o run -- python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline ;;
         pmc-fetch) step pmc_fetch 600 rocprofv3 --pmc FETCH_SIZE --output-format csv -d gpurun_out/pmc_fetch -o run -- python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline --batch 2 ;;
         pmc-write) step pmc_write 600 rocprofv3 --pmc WRITE_SIZE --output-format csv -d gpurun_out/pmc_write -o run -- python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline --batch 2 ;;
+        stream) step stream 300 python3 tools/stream_hbm.py ;;
+        pmc-cost-sq) step pmc_cost_sq 600 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_INSTS_VALU SQ_WAIT_INST_LDS --kernel-include-regex cost_walk --output-format csv -d gpurun_out/pmc_cost_sq -o run -- python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline --batch 2 --concurrency 1 ;;
+        pmc-cost-lds) step pmc_cost_lds 600 rocprofv3 --pmc SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_INSTS_LDS SQ_INSTS_VMEM_WR SQ_INSTS_VMEM_RD SQ_ACTIVE_INST_LDS SQ_INSTS_SALU SQ_WAVES --kernel-include-regex cost_walk --output-format csv -d gpurun_out/pmc_cost_lds -o run -- python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline --batch 2 --concurrency 1 ;;
+        pmc-cost-write) step pmc_cost_write 600 rocprofv3 --pmc WRITE_SIZE --kernel-include-regex cost_walk --output-format csv -d gpurun_out/pmc_cost_write -o run -- python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline --batch 2 --concurrency 1 ;;
+        pmc-cost-fetch) step pmc_cost_fetch 600 rocprofv3 --pmc FETCH_SIZE --kernel-include-regex cost_walk --output-format csv -d gpurun_out/pmc_cost_fetch -o run -- python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline --batch 2 --concurrency 1 ;;
         *) echo "unknown step $s"; exit 2 ;;
     esac
 done
