@@ -10,6 +10,8 @@
 // input vector is read from HBM once per pass and the pass runs IN PLACE.  A wave owns
 // one output pixel at a time: the arm lengths are wave-uniform, lanes own 4 consecutive
 // disparities and every LDS read is one conflict-free ds_read_b128 per lane.
+#include <stdlib.h>
+
 #include "tsm_device.h"
 #include "tsm_launch.h"
 
@@ -263,6 +265,207 @@ __global__ __launch_bounds__(AG_THREADS) void k_agg_line(float* __restrict__ vol
     }
 }
 
+// ---------------------------------------------------------------------------
+// 1-D aggregation v3: LDS-DMA line streamer (one loader wave + 8 summing waves)
+// ---------------------------------------------------------------------------
+// The pass is bound by how many bytes each CU keeps in flight, not by arithmetic.
+// A workgroup owns one line; the line's pixel vectors stream into an LDS ring in chunks
+// of AGD_SEG pixels by LDS-DMA (global_load_lds_dwordx4, no registers), issued by a
+// dedicated loader wave D chunks ahead of the chunk being summed, so ~D*AGD_SEG vectors
+// (tens of KB per CU) are always in flight.  The ring holds the 2*AH+1 chunks a step's
+// windows can touch (AH = ceil(A / AGD_SEG) halo chunks per side) plus the D in flight.
+// The loader alone waits on its DMAs (a counted vmcnt, younger DMAs stay in flight),
+// then the step barrier publishes the chunk; summing waves never wait on memory.  Each
+// summing wave produces AGD_OPW outputs per step with the sequential window sum of the
+// reference (lanes own float4 of labels).  In place: an output overwrites pixel p only
+// after the chunk holding p was staged, and later windows read p from the ring.
+constexpr int AGD_SEG = 16;                     // pixels per chunk = outputs per step
+constexpr int AGD_SUM_WAVES = 8;
+constexpr int AGD_OPW = AGD_SEG / AGD_SUM_WAVES;  // outputs per summing wave per step
+constexpr int AGD_THREADS = (AGD_SUM_WAVES + 1) * 64;
+constexpr int AGD_MAX_RING = 32;                // chunks
+
+// s_waitcnt vmcnt(n) for a runtime n, rounded DOWN to a multiple of 8 (waiting for a few
+// more operations than needed is safe) so the dispatch is a short branch tree
+__device__ __forceinline__ void wait_vmcnt(int n) {
+    n = n > 63 ? 63 : n;
+    switch (n >> 3) {
+        case 7: asm volatile("s_waitcnt vmcnt(56)" ::: "memory"); break;
+        case 6: asm volatile("s_waitcnt vmcnt(48)" ::: "memory"); break;
+        case 5: asm volatile("s_waitcnt vmcnt(40)" ::: "memory"); break;
+        case 4: asm volatile("s_waitcnt vmcnt(32)" ::: "memory"); break;
+        case 3: asm volatile("s_waitcnt vmcnt(24)" ::: "memory"); break;
+        case 2: asm volatile("s_waitcnt vmcnt(16)" ::: "memory"); break;
+        case 1: asm volatile("s_waitcnt vmcnt(8)" ::: "memory"); break;
+        default: asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); break;
+    }
+}
+
+#ifdef TSM_EXP_STAMPS
+__device__ unsigned long long g_agg_stamps[8192 * 9 * 4];  // [block][wave][total, vmwait, barrier, work]
+#endif
+
+template <int J>
+__global__ __launch_bounds__(AGD_THREADS) void k_agg_dma(float* __restrict__ vol,
+                                                         const uint32_t* __restrict__ arms,
+                                                         const int32_t* __restrict__ ws,
+                                                         int horizontal, int A, int RC, int D,
+                                                         DevParams Pk) {
+    const DevParams P = Pk;  // kernel args -> registers once (no per-use kernarg reloads)
+    extern __shared__ __attribute__((aligned(16))) f32x4 smem_f4[];
+    const int H = P.H, W = P.W, Lp = P.Lp;
+    const int Q = Lp >> 2;                          // float4 per pixel vector
+    const int CS = AGD_SEG * Q;                     // float4 per ring chunk (exact: pixel-linear ring)
+    const int ndma = CS >> 6;                       // DMA instructions per chunk
+    const int AH = (A + AGD_SEG - 1) / AGD_SEG;     // halo chunks per side
+    const int v = blockIdx.y;
+    const int line = blockIdx.x;
+    const int n = horizontal ? W : H;
+    const size_t es = horizontal ? (size_t)Lp : (size_t)W * Lp;  // floats between neighbours
+    float* base = vol + (size_t)v * H * W * Lp + (horizontal ? (size_t)line * W * Lp : (size_t)line * Lp);
+    const uint32_t* ab = arms + (size_t)v * H * W + (horizontal ? (size_t)line * W : (size_t)line);
+    const size_t as = horizontal ? 1 : (size_t)W;
+    const int32_t* wsl = ws ? ws + (size_t)v * 2 * H * W + (horizontal ? (size_t)line * W : (size_t)line) : nullptr;
+    const int shA = horizontal ? 16 : 0, shB = horizontal ? 24 : 8;
+    f32x4* ring = smem_f4;
+    uint32_t* arm_s = reinterpret_cast<uint32_t*>(ring + (size_t)RC * CS + 4 * Q + 64 * J);
+    float* ws_s = reinterpret_cast<float*>(arm_s + n);
+
+    const int tid = threadIdx.x;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int lane = tid & 63;
+    const int nchunks = (n + AGD_SEG - 1) / AGD_SEG;
+    const bool loader = wave == AGD_SUM_WAVES;
+
+    // loader: DMA chunk c (pixels c*SEG ..) into ring slot c % RC; the ring is pixel-
+    // linear (pixel p at (p mod RC*SEG) * Q).  Instruction k moves chunk float4
+    // f = 64 k + lane (pixel f / Q, group f % Q); the last one runs with only the lanes
+    // that still hold chunk data active, so no DMA writes outside its chunk.  Pixels
+    // past the line end re-read a valid vector into slots nobody reads.  Per-lane
+    // offsets are computed once (no per-step divisions).
+    constexpr int KMAX = AGD_SEG * J;  // ndma <= SEG * ceil(Q / 64)
+    int pxo[KMAX];
+    uint32_t gofs[KMAX];
+#pragma unroll
+    for (int k = 0; k < KMAX; ++k) {
+        const int f = k * 64 + lane;
+        const bool data = f < AGD_SEG * Q;
+        pxo[k] = data ? f / Q : 0;
+        gofs[k] = data ? 4u * (uint32_t)(f - (f / Q) * Q) : 0u;
+    }
+    const bool last_lane_ok = (ndma - 1) * 64 + lane < CS;
+    auto dma_chunk = [&](int c) {
+        f32x4* slot = ring + (size_t)(c % RC) * CS;
+#pragma unroll
+        for (int k = 0; k < KMAX; ++k) {
+            if (k < ndma && (k < ndma - 1 || last_lane_ok)) {
+                int px = c * AGD_SEG + pxo[k];
+                px = px < n ? px : n - 1;
+                const float* src = base + (size_t)px * es + gofs[k];
+                __builtin_amdgcn_global_load_lds(src, slot + k * 64, 16, 0, 0);
+            }
+        }
+    };
+    if (loader) {
+        for (int c = 0; c < AH + D; ++c) dma_chunk(c);  // chunks past the end: dead slots
+    }
+    for (int i = tid; i < n; i += AGD_THREADS) {
+        const uint32_t a = ab[(size_t)i * as];
+        arm_s[i] = (((a >> shA) & 0xffu) << 16) | ((a >> shB) & 0xffu);  // lo<<16 | hi
+        if (wsl) ws_s[i] = (float)wsl[(size_t)i * as];
+    }
+    __syncthreads();  // arms / window sizes staged (full fence: LDS writes visible)
+#ifdef TSM_EXP_STAMPS
+    unsigned long long t_start = __builtin_amdgcn_s_memtime(), t_vm = 0, t_bar = 0, t_work = 0;
+#define AGS(x) unsigned long long x = __builtin_amdgcn_s_memtime()
+#else
+#define AGS(x)
+#endif
+    for (int s = 0; s < nchunks; ++s) {
+        AGS(ta);
+        if (loader) wait_vmcnt((D - 1) * ndma);  // chunk s+AH landed (D-1 younger chunks fly)
+        AGS(tb);
+        // bare s_barrier, NOT __syncthreads(): its fence would drain every wave's vmcnt,
+        // i.e. wait for all DMAs in flight and serialise the stream.  Summing waves
+        // write no LDS, and their ring reads of step s-1 have returned before they
+        // arrive here, so chunk s-AH-1's slot is free for the next DMA.
+        __builtin_amdgcn_s_barrier();
+        AGS(tc);
+#ifdef TSM_EXP_STAMPS
+        t_vm += tb - ta;
+        t_bar += tc - tb;
+#endif
+        if (loader) {
+            dma_chunk(s + AH + D);               // into the slot of chunk s-AH-1
+        } else {
+#pragma unroll
+            for (int u = 0; u < AGD_OPW; ++u) {
+                const int o = s * AGD_SEG + u * AGD_SUM_WAVES + wave;
+                if (o >= n) break;
+                const uint32_t a = arm_s[o];
+                const int lo = (int)(a >> 16), hi = (int)(a & 0xffffu);
+                f32x4 acc[J];
+#pragma unroll
+                for (int j = 0; j < J; ++j) acc[j] = f32x4{0.f, 0.f, 0.f, 0.f};
+                // Window [o-lo, o+hi] in at most two runs of the pixel-linear ring (it wraps
+                // once at most), summed strictly in window order in blocks of 4 reads;
+                // a block's reads past the run end add +0.0 (exact: sums are >= +0).
+                // Every lane reads (lanes >= Q read neighbouring ring data, never stored).
+                const int RP = RC * AGD_SEG;
+                int p = (o - lo) % RP;
+                int len = lo + hi + 1;
+                for (int run = 0; run < 2 && len > 0; ++run) {
+                    const int rl = min(len, RP - p);
+                    const f32x4* r = ring + (size_t)p * Q + lane;
+                    for (int i = 0; i < rl; i += 4) {
+                        f32x4 x[4][J];
+#pragma unroll
+                        for (int u = 0; u < 4; ++u)
+#pragma unroll
+                            for (int j = 0; j < J; ++j) x[u][j] = r[(i + u) * Q + 64 * j];
+#pragma unroll
+                        for (int u = 0; u < 4; ++u) {
+                            const bool in = i + u < rl;
+#pragma unroll
+                            for (int j = 0; j < J; ++j) {
+                                acc[j].x += in ? x[u][j].x : 0.f;
+                                acc[j].y += in ? x[u][j].y : 0.f;
+                                acc[j].z += in ? x[u][j].z : 0.f;
+                                acc[j].w += in ? x[u][j].w : 0.f;
+                            }
+                        }
+                    }
+                    len -= rl;
+                    p = 0;
+                }
+                if (wsl) {
+                    const float wsz = ws_s[o];
+#pragma unroll
+                    for (int j = 0; j < J; ++j) acc[j] /= wsz;
+                }
+#pragma unroll
+                for (int j = 0; j < J; ++j) {
+                    const int q = lane + 64 * j;
+                    if (q < Q) *reinterpret_cast<f32x4*>(base + (size_t)o * es + 4 * q) = acc[j];
+                }
+            }
+        }
+#ifdef TSM_EXP_STAMPS
+        { AGS(td); t_work += td - tc; }
+#endif
+    }
+    if (loader) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // no DMA outlives the WG
+#ifdef TSM_EXP_STAMPS
+    {
+        const size_t bid = (size_t)blockIdx.y * gridDim.x + blockIdx.x;
+        if (lane == 0 && bid < 8192) {
+            unsigned long long* o = g_agg_stamps + (bid * 9 + wave) * 4;
+            o[0] = __builtin_amdgcn_s_memtime() - t_start; o[1] = t_vm; o[2] = t_bar; o[3] = t_work;
+        }
+    }
+#endif
+}
+
 void launch_arms(const uint32_t* img, uint32_t* arms, const DevParams& P, hipStream_t st) {
     dim3 g((P.W + 127) / 128, P.H, 2);
     hipLaunchKernelGGL(k_arms, g, dim3(128), 0, st, img, arms, P); trace_point("k_arms", st);
@@ -285,19 +488,62 @@ size_t agg_lds_bytes(const DevParams& P) {
     return (size_t)(AG_SEG + 2 * A) * (P.Lp / 4) * 16 + (size_t)nmax * 8;
 }
 
+// Ring geometry of the DMA streamer: returns the LDS bytes and sets RC / D, or 0 when
+// fewer than 2 chunks could be in flight (the register-staged kernel is used then).
+static size_t agg_dma_geometry(const DevParams& P, int& RC, int& D) {
+    const int A = P.max_length1 - 1;
+    const int Q = P.Lp / 4;
+    const int CS = AGD_SEG * Q;
+    const int AH = (A + AGD_SEG - 1) / AGD_SEG;
+    const int nmax = P.W > P.H ? P.W : P.H;
+    // arms / window sizes, plus the tail pad a block of reads may touch past the ring
+    // end (4 pixel vectors and 64 lanes per float4 group)
+    const size_t fixed = (size_t)nmax * 8 + (size_t)(4 * Q + 64 * ((Q + 63) / 64)) * 16;
+    const size_t chunk = (size_t)CS * 16;
+    if (fixed >= 160 * 1024) return 0;
+    int rc = (int)((160 * 1024 - fixed) / chunk);
+    rc = rc > AGD_MAX_RING ? AGD_MAX_RING : rc;
+    static const int dcap = [] {
+        const char* e = getenv("TSM_AGG_D");  // tuning override: chunks in flight
+        return e ? atoi(e) : 0;
+    }();
+    if (dcap >= 2 && rc > 2 * AH + 1 + dcap) rc = 2 * AH + 1 + dcap;
+    D = rc - (2 * AH + 1);
+    if (D < 2) return 0;
+    RC = rc;
+    return (size_t)rc * chunk + fixed;
+}
+
 int launch_agg_line(float* vol, const uint32_t* arms, const int32_t* ws, int horizontal,
                     const DevParams& P, hipStream_t st) {
     const int A = P.max_length1 - 1;
     const int J = (P.Lp / 4 + 63) / 64;
     dim3 g(horizontal ? P.H : P.W, 2);
-    const size_t lds = agg_lds_bytes(P);
-    if (lds > 160 * 1024) return -1;
     static bool attr_set = false;
     if (!attr_set) {
         hipFuncSetAttribute((const void*)k_agg_line<1>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
         hipFuncSetAttribute((const void*)k_agg_line<2>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+        hipFuncSetAttribute((const void*)k_agg_dma<1>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+        hipFuncSetAttribute((const void*)k_agg_dma<2>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
         attr_set = true;
     }
+    static const bool use_dma = [] {
+        const char* e = getenv("TSM_AGG_KERNEL");  // tuning override: "line" = register-staged
+        return !(e && e[0] == 'l');
+    }();
+    int RC = 0, D = 0;
+    const size_t lds_dma = use_dma ? agg_dma_geometry(P, RC, D) : 0;
+    if (lds_dma) {
+        switch (J) {
+            case 1: hipLaunchKernelGGL((k_agg_dma<1>), g, dim3(AGD_THREADS), lds_dma, st, vol, arms, ws, horizontal, A, RC, D, P); break;
+            case 2: hipLaunchKernelGGL((k_agg_dma<2>), g, dim3(AGD_THREADS), lds_dma, st, vol, arms, ws, horizontal, A, RC, D, P); break;
+            default: return -1;
+        }
+        trace_point("k_agg_dma", st);
+        return 0;
+    }
+    const size_t lds = agg_lds_bytes(P);
+    if (lds > 160 * 1024) return -1;
     switch (J) {
         case 1: hipLaunchKernelGGL((k_agg_line<1>), g, dim3(AG_THREADS), lds, st, vol, arms, ws, horizontal, A, P); break;
         case 2: hipLaunchKernelGGL((k_agg_line<2>), g, dim3(AG_THREADS), lds, st, vol, arms, ws, horizontal, A, P); break;
@@ -308,3 +554,9 @@ int launch_agg_line(float* vol, const uint32_t* arms, const int32_t* ws, int hor
 }
 
 }  // namespace tsm
+
+#ifdef TSM_EXP_STAMPS
+extern "C" int tsm_exp_agg_stamps(void* host, size_t bytes) {
+    return (int)hipMemcpyFromSymbol(host, HIP_SYMBOL(tsm::g_agg_stamps), bytes, 0, hipMemcpyDeviceToHost);
+}
+#endif
