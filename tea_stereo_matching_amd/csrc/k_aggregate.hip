@@ -316,7 +316,7 @@ __global__ __launch_bounds__(AGD_THREADS) void k_agg_dma(float* __restrict__ vol
     const int H = P.H, W = P.W, Lp = P.Lp;
     const int Q = Lp >> 2;                          // float4 per pixel vector
     const int CS = AGD_SEG * Q;                     // float4 per ring chunk (exact: pixel-linear ring)
-    const int ndma = CS >> 6;                       // DMA instructions per chunk
+    const int ndma = (CS + 63) >> 6;                // DMA instructions per chunk
     const int AH = (A + AGD_SEG - 1) / AGD_SEG;     // halo chunks per side
     const int v = blockIdx.y;
     const int line = blockIdx.x;
