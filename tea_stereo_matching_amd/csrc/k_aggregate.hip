@@ -266,23 +266,24 @@ __global__ __launch_bounds__(AG_THREADS) void k_agg_line(float* __restrict__ vol
 }
 
 // ---------------------------------------------------------------------------
-// 1-D aggregation v3: LDS-DMA line streamer (one loader wave + 8 summing waves)
+// 1-D aggregation v3: LDS-DMA line streamer (1 loader wave + 12 summing waves)
 // ---------------------------------------------------------------------------
 // The pass is bound by how many bytes each CU keeps in flight, not by arithmetic.
 // A workgroup owns one line; the line's pixel vectors stream into an LDS ring in chunks
 // of AGD_SEG pixels by LDS-DMA (global_load_lds_dwordx4, no registers), issued by a
-// dedicated loader wave D chunks ahead of the chunk being summed, so ~D*AGD_SEG vectors
+// dedicated loader waves D chunks ahead of the chunk being summed, so ~D*AGD_SEG vectors
 // (tens of KB per CU) are always in flight.  The ring holds the 2*AH+1 chunks a step's
 // windows can touch (AH = ceil(A / AGD_SEG) halo chunks per side) plus the D in flight.
-// The loader alone waits on its DMAs (a counted vmcnt, younger DMAs stay in flight),
+// Each loader waits only on its own DMAs (a counted vmcnt, younger DMAs stay in flight),
 // then the step barrier publishes the chunk; summing waves never wait on memory.  Each
 // summing wave produces AGD_OPW outputs per step with the sequential window sum of the
 // reference (lanes own float4 of labels).  In place: an output overwrites pixel p only
 // after the chunk holding p was staged, and later windows read p from the ring.
-constexpr int AGD_SEG = 16;                     // pixels per chunk = outputs per step
-constexpr int AGD_SUM_WAVES = 8;
-constexpr int AGD_OPW = AGD_SEG / AGD_SUM_WAVES;  // outputs per summing wave per step
-constexpr int AGD_THREADS = (AGD_SUM_WAVES + 1) * 64;
+constexpr int AGD_SUM_WAVES = 12;
+constexpr int AGD_LOAD_WAVES = 1;               // DMA issue is slow per wave: spread it
+constexpr int AGD_OPW = 1;                      // outputs per summing wave per step
+constexpr int AGD_SEG = AGD_SUM_WAVES * AGD_OPW;  // pixels per chunk = outputs per step
+constexpr int AGD_THREADS = (AGD_SUM_WAVES + AGD_LOAD_WAVES) * 64;
 constexpr int AGD_MAX_RING = 32;                // chunks
 
 // s_waitcnt vmcnt(n) for a runtime n, rounded DOWN to a multiple of 8 (waiting for a few
@@ -335,7 +336,10 @@ __global__ __launch_bounds__(AGD_THREADS) void k_agg_dma(float* __restrict__ vol
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int lane = tid & 63;
     const int nchunks = (n + AGD_SEG - 1) / AGD_SEG;
-    const bool loader = wave == AGD_SUM_WAVES;
+    const bool loader = wave >= AGD_SUM_WAVES;
+    const int li = wave - AGD_SUM_WAVES;            // loader index (valid when loader)
+    // this loader's DMA instructions of a chunk: k = li, li + NLOAD, ... < ndma
+    const int nmine = loader ? (ndma - li + AGD_LOAD_WAVES - 1) / AGD_LOAD_WAVES : 0;
 
     // loader: DMA chunk c (pixels c*SEG ..) into ring slot c % RC; the ring is pixel-
     // linear (pixel p at (p mod RC*SEG) * Q).  Instruction k moves chunk float4
@@ -343,11 +347,12 @@ __global__ __launch_bounds__(AGD_THREADS) void k_agg_dma(float* __restrict__ vol
     // that still hold chunk data active, so no DMA writes outside its chunk.  Pixels
     // past the line end re-read a valid vector into slots nobody reads.  Per-lane
     // offsets are computed once (no per-step divisions).
-    constexpr int KMAX = AGD_SEG * J;  // ndma <= SEG * ceil(Q / 64)
+    constexpr int KMAX = (AGD_SEG * J + AGD_LOAD_WAVES - 1) / AGD_LOAD_WAVES;  // per loader
     int pxo[KMAX];
     uint32_t gofs[KMAX];
 #pragma unroll
-    for (int k = 0; k < KMAX; ++k) {
+    for (int m = 0; m < KMAX; ++m) {
+        const int k = li + AGD_LOAD_WAVES * m;
         const int f = k * 64 + lane;
         const bool data = f < AGD_SEG * Q;
         pxo[k] = data ? f / Q : 0;
@@ -357,11 +362,12 @@ __global__ __launch_bounds__(AGD_THREADS) void k_agg_dma(float* __restrict__ vol
     auto dma_chunk = [&](int c) {
         f32x4* slot = ring + (size_t)(c % RC) * CS;
 #pragma unroll
-        for (int k = 0; k < KMAX; ++k) {
-            if (k < ndma && (k < ndma - 1 || last_lane_ok)) {
-                int px = c * AGD_SEG + pxo[k];
+        for (int m = 0; m < KMAX; ++m) {
+            const int k = li + AGD_LOAD_WAVES * m;
+            if (m < nmine && (k < ndma - 1 || last_lane_ok)) {
+                int px = c * AGD_SEG + pxo[m];
                 px = px < n ? px : n - 1;
-                const float* src = base + (size_t)px * es + gofs[k];
+                const float* src = base + (size_t)px * es + gofs[m];
                 __builtin_amdgcn_global_load_lds(src, slot + k * 64, 16, 0, 0);
             }
         }
@@ -383,7 +389,7 @@ __global__ __launch_bounds__(AGD_THREADS) void k_agg_dma(float* __restrict__ vol
 #endif
     for (int s = 0; s < nchunks; ++s) {
         AGS(ta);
-        if (loader) wait_vmcnt((D - 1) * ndma);  // chunk s+AH landed (D-1 younger chunks fly)
+        if (loader) wait_vmcnt((D - 1) * nmine);  // my part of chunk s+AH landed (D-1 younger chunks fly)
         AGS(tb);
         // bare s_barrier, NOT __syncthreads(): its fence would drain every wave's vmcnt,
         // i.e. wait for all DMAs in flight and serialise the stream.  Summing waves
