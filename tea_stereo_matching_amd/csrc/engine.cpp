@@ -13,6 +13,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <string>
+#include <limits>
 #include <vector>
 
 #include "../../include/tsm_adcensus.h"
@@ -98,6 +99,7 @@ struct Workspace {
     float* vol = nullptr;          // [2][H][W][Lp]
     uint32_t* arms = nullptr;      // [2][H][W]
     uint32_t* cost_ctr = nullptr;  // cost-walk unit counter (never reset, see k_cost.hip)
+    float* infvec = nullptr;       // 64 x +inf (scanline lanes past the label axis)
     uint32_t cost_ctr_base = 0;
     int32_t* ws = nullptr;         // [2][2][H][W]
     uint8_t* gv = nullptr;         // [2][H][gstride] (sentinel margins)
@@ -278,6 +280,7 @@ int ensure_workspace(tsm_adc* h, Workspace* w, int H, int W) {
     A(w->vol, 2 * N * (size_t)Lp * 4);
     A(w->arms, 2 * N * 4);
     A(w->cost_ctr, 256);
+    A(w->infvec, 256);
     A(w->ws, 4 * N * 4);
     {
         const int gp = grad_pad(h->max_disparity);
@@ -321,6 +324,10 @@ int ensure_workspace(tsm_adc* h, Workspace* w, int H, int W) {
     // padded lanes of the volume are never read as labels; keep them defined anyway
     HIP_OK(hipMemset(w->vol, 0, 2 * N * (size_t)Lp * 4));
     HIP_OK(hipMemset(w->cost_ctr, 0, 256));
+    {
+        std::vector<float> inf(64, std::numeric_limits<float>::infinity());
+        HIP_OK(hipMemcpy(w->infvec, inf.data(), 256, hipMemcpyHostToDevice));
+    }
     w->cost_ctr_base = 0;
     w->H = H;
     w->W = W;
@@ -461,10 +468,10 @@ int run_pipeline(tsm_adc* h, Workspace* w, const uint8_t* d_left, const uint8_t*
     if (dump && dump->cost_agg && (rc = dump_vol(dump->cost_agg, 2)) != TSM_OK) return rc;
     // --- scanline (+ fused WTA in the last pass) -------------------------------------
     const bool keep_view1 = dump && dump->cost_scan;
-    if (launch_scan_vertical(w->vol, w->gv, w->img, +1, P, st) != 0 ||
-        launch_scan_vertical(w->vol, w->gv, w->img, -1, P, st) != 0 ||
-        launch_scan_horizontal(w->vol, w->gh, w->img, +1, nullptr, 1, P, st) != 0 ||
-        launch_scan_horizontal(w->vol, w->gh, w->img, -1, w->rb.disp0, keep_view1 ? 1 : 0, P, st) != 0)
+    if (launch_scan_vertical(w->vol, w->gv, w->img, +1, w->infvec, P, st) != 0 ||
+        launch_scan_vertical(w->vol, w->gv, w->img, -1, w->infvec, P, st) != 0 ||
+        launch_scan_horizontal(w->vol, w->gh, w->img, +1, nullptr, 1, w->infvec, P, st) != 0 ||
+        launch_scan_horizontal(w->vol, w->gh, w->img, -1, w->rb.disp0, keep_view1 ? 1 : 0, w->infvec, P, st) != 0)
         return fail(h, TSM_ERR_UNSUPPORTED, "scanline: label count");
     mark();
     if (keep_view1 && (rc = dump_vol(dump->cost_scan, 2)) != TSM_OK) return rc;

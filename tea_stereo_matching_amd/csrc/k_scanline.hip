@@ -112,7 +112,7 @@ __device__ __forceinline__ ScanConst scan_const(const DevParams& P) {
 // Prefetched, chain-independent inputs of one step.
 template <int J>
 struct StepIn {
-    f32x4 p[J];      // this pixel's L-vector (padding and lanes >= Q: +inf)
+    f32x4 p[J];      // this pixel's L-vector (lanes >= Q: a constant +inf vector)
     uint32_t g0[J];  // aligned 8-byte window of the other view's colour differences
     uint32_t g1[J];
     int d1;          // own-view colour difference to the predecessor
@@ -126,43 +126,41 @@ __device__ __forceinline__ uint32_t d2_bytes(uint32_t lo, uint32_t hi, uint32_t 
     return rev ? __builtin_amdgcn_perm(w, w, 0x00010203u) : w;
 }
 
-template <int J, bool HORIZ>
-__device__ __forceinline__ void scan_issue(StepIn<J>& s, int it, int len, int dir, int line,
-                                           const float* base, size_t es, const uint8_t* gown,
-                                           const uint8_t* goth, const uint32_t* im, bool mask,
-                                           int sgn, int lane, const ScanConst& C) {
-    const int pos = dir > 0 ? 1 + it : len - 2 - it;  // w1 (HORIZ) or h1 (vertical)
-    const int pm = dir > 0 ? pos : pos + 1;            // max(pos, predecessor)
-    const float* ptr = base + (size_t)pos * es;
+// Per-lane addressing, fixed for the whole walk: the vector element of lane q lives at
+// vbase + pos * ves (lanes >= Q: ves = 0 on a +inf vector, so no per-step select), its
+// d2 bytes at dbase + pos * dstep (8-byte aligned window, sentinel-padded map).
+template <int J>
+struct LaneAddr {
+    const float* vb[J];
+    size_t ves[J];
+    int gb[J];  // byte offset of this lane's 4-byte d2 group relative to x0 (aligned later)
+};
+
+template <int J, bool HORIZ, bool MASK>
+__device__ __forceinline__ void scan_issue(StepIn<J>& s, int pos, int dir, int line,
+                                           const LaneAddr<J>& la, const uint8_t* gown,
+                                           const uint8_t* goth, const uint32_t* im,
+                                           int sgn, const ScanConst& C) {
+    const int pm = dir > 0 ? pos : pos + 1;  // max(pos, predecessor)
 #pragma unroll
-    for (int j = 0; j < J; ++j) {
-        const int q = lane + 64 * j;
-        const int qc = q < C.Q ? q : C.Q - 1;  // clamped, always-valid address
-        const f32x4 v = *reinterpret_cast<const f32x4*>(ptr + 4 * qc);
-        const float inf = bitsf(kInfBits);
-        s.p[j] = q < C.Q ? v : f32x4{inf, inf, inf, inf};
-    }
+    for (int j = 0; j < J; ++j) s.p[j] = *reinterpret_cast<const f32x4*>(la.vb[j] + (size_t)pos * la.ves[j]);
     // d1 / mask loads: wave-uniform addresses laundered into a VGPR, so they are
     // vector loads ordered by vmcnt (a scalar load would need lgkmcnt(0) at its use)
     int i1 = HORIZ ? C.gpad + pm : pm * C.gstride + C.gpad + line;
     asm volatile("v_mov_b32 %0, %1" : "=v"(i1) : "v"(i1));
     s.d1 = gown[i1];
     s.mk = 1u;
-    if (mask) {
+    if (MASK) {
         int im_idx = HORIZ ? line * C.W + (pos - dir) : (pos - dir) * C.W + line;
         asm volatile("v_mov_b32 %0, %1" : "=v"(im_idx) : "v"(im_idx));
         s.mk = im[im_idx];
     }
-    // x of this lane's first disparity; HORIZ reads byte max(x1, x2) = x1 + (dir < 0)
+    // x of lane 0's first disparity; HORIZ reads byte max(x1, x2) = x1 + (dir < 0)
     const uint8_t* grow = HORIZ ? goth : goth + (size_t)pm * C.gstride;
     const int x0 = (HORIZ ? pos + (dir < 0 ? 1 : 0) : line) + C.gpad + sgn * C.minD;
 #pragma unroll
     for (int j = 0; j < J; ++j) {
-        // bytes [b, b+4): view 0 b = x0 + 4q, view 1 b = x0 - 4q - 3 (then reversed)
-        const int q = lane + 64 * j;
-        const int b = sgn > 0 ? x0 + 4 * q : x0 - 4 * q - 3;
-        const int bc = b < 0 ? 0 : (b > C.gstride - 8 ? C.gstride - 8 : b);  // lanes past the vector
-        const uint2 w = *reinterpret_cast<const uint2*>(grow + (bc & ~3));
+        const uint2 w = *reinterpret_cast<const uint2*>(grow + ((x0 + la.gb[j]) & ~3));
         s.g0[j] = w.x;
         s.g1[j] = w.y;
     }
@@ -178,10 +176,12 @@ __device__ __forceinline__ void partial_opt(f32x4 (&p)[J], const f32x4 (&q)[J], 
     const bool sim1 = d1 < C.cd;
     const float p1a = sim1 ? C.p1[2] : C.p1[1], p1b = sim1 ? C.p1[1] : C.p1[0];
     const float p2a = sim1 ? C.p2[2] : C.p2[1], p2b = sim1 ? C.p2[1] : C.p2[0];
+    const float m2a = mqf + p2a, m2b = mqf + p2b;  // m + P2 for both classes
     const float inf = bitsf(kInfBits);
 #pragma unroll
     for (int j = 0; j < J; ++j) {
-        // d-1 of element 0 / d+1 of element 3 from the neighbouring lanes (+inf at the ends)
+        // d-1 of element 0 / d+1 of element 3 from the neighbouring lanes (+inf past the
+        // ends of the label axis: lanes >= Q hold the +inf vector, DPP feeds +inf at 0/63)
         float lo = dpp_f<DPP_WAVE_SHR1>(q[j][3], inf);
         float hi = dpp_f<DPP_WAVE_SHL1>(q[j][0], inf);
         if (j > 0) {
@@ -199,10 +199,10 @@ __device__ __forceinline__ void partial_opt(f32x4 (&p)[J], const f32x4 (&q)[J], 
         for (int k = 0; k < 4; ++k) {
             const bool sim2 = (int)((g >> (8 * k)) & 0xffu) < C.cd;
             const float p1 = sim2 ? p1a : p1b;
-            const float p2 = sim2 ? p2a : p2b;
+            const float m2 = sim2 ? m2a : m2b;
             const float cost = pe[k] - mqf;
             // min{ m + P2, C(q,d), C(q,d-1) + P1, C(q,d+1) + P1 } (all >= 0: integer min)
-            const uint32_t mo = umin3(min(fbits(mqf + p2), fbits(qe[k + 1])), fbits(qe[k] + p1),
+            const uint32_t mo = umin3(min(fbits(m2), fbits(qe[k + 1])), fbits(qe[k] + p1),
                                       fbits(qe[k + 2] + p1));
             pe[k] = (cost + bitsf(mo)) * 0.5f;  // == / 2 exactly
         }
@@ -212,16 +212,25 @@ __device__ __forceinline__ void partial_opt(f32x4 (&p)[J], const f32x4 (&q)[J], 
 
 // ---------------------------------------------------------------------------
 // One wave walks one line of one view.  The leftward horizontal pass is the last one:
-// it emits the WTA disparity of every pixel and, for view 1 (only needed for the WTA),
-// can skip storing the volume.
+// it emits the WTA disparity of every pixel (WTA) and, for view 1 (only needed for the
+// WTA), can skip storing the volume.  MASK: mask-mode predecessor test.  The racy
+// omp schedule emulation costs two scalar compares per step (chunk starts are tracked
+// incrementally).
 // ---------------------------------------------------------------------------
 constexpr int SC_K = 8;  // prefetch depth (steps)
 
-template <int J, bool HORIZ>
+// first iteration of omp-static chunk t (libgomp / vcomp: first n%T threads take q+1)
+__device__ __forceinline__ int omp_start(int t, int n, int T) {
+    const int q = n / T, r = n % T;
+    return t * q + (t < r ? t : r);
+}
+
+template <int J, bool HORIZ, bool MASK, bool WTA>
 __global__ __launch_bounds__(256) void k_scan_line(float* __restrict__ vol,
                                                    const uint8_t* __restrict__ grad,
                                                    const uint32_t* __restrict__ img, int dir,
                                                    int32_t* __restrict__ wta, int store_view1,
+                                                   const float* __restrict__ infvec,
                                                    DevParams Pk) {
     const DevParams P = Pk;
     const int H = P.H, W = P.W, Lp = P.Lp;
@@ -236,29 +245,31 @@ __global__ __launch_bounds__(256) void k_scan_line(float* __restrict__ vol,
     const uint8_t* gown = grad + (size_t)v * H * C.gstride + (HORIZ ? (size_t)line * C.gstride : 0);
     const uint8_t* goth = grad + (size_t)(1 - v) * H * C.gstride + (HORIZ ? (size_t)line * C.gstride : 0);
     const uint32_t* im = img + (size_t)v * H * W;
-    const bool mask = P.mask != 0;
     const int sgn = v == 0 ? 1 : -1;
     const bool rev = sgn < 0;
     const int n = len - 1;
     const int T = P.omp_threads;
-    const bool store = !(wta && v == 1 && !store_view1);
-    int32_t* wrow = wta ? wta + ((size_t)v * H + line) * W : nullptr;  // only HORIZ passes emit WTA
+    const bool store = !(WTA && v == 1 && !store_view1);
+    int32_t* wrow = WTA ? wta + ((size_t)v * H + line) * W : nullptr;
     // byte misalignment of every lane's d2 window (uniform: lanes differ by multiples of 4)
     const int x0a = (HORIZ ? (dir < 0 ? 1 : 0) : line) + C.gpad + sgn * C.minD - (sgn > 0 ? 0 : 3);
     const int posbase = dir > 0 ? 1 : len - 2;  // pos(it) = posbase + dir*it (HORIZ shifts x0)
+    LaneAddr<J> la;
+#pragma unroll
+    for (int j = 0; j < J; ++j) {
+        const int q = lane + 64 * j;
+        const bool in = q < C.Q;
+        la.vb[j] = in ? base + 4 * q : infvec;
+        la.ves[j] = in ? es : 0;
+        la.gb[j] = in ? (sgn > 0 ? 4 * q : -4 * q - 3) : 0;
+    }
 
     f32x4 q[J];
     const int p0 = dir > 0 ? 0 : len - 1;
 #pragma unroll
-    for (int j = 0; j < J; ++j) {
-        const int qq = lane + 64 * j;
-        const int qc = qq < C.Q ? qq : C.Q - 1;
-        const f32x4 v0 = *reinterpret_cast<const f32x4*>(base + (size_t)p0 * es + 4 * qc);
-        const float inf = bitsf(kInfBits);
-        q[j] = qq < C.Q ? v0 : f32x4{inf, inf, inf, inf};
-    }
+    for (int j = 0; j < J; ++j) q[j] = *reinterpret_cast<const f32x4*>(la.vb[j] + (size_t)p0 * la.ves[j]);
     uint32_t mq = vec_min_bits<J>(q);
-    if (wrow) {
+    if (WTA) {
         const int d = vec_argmin<J>(q, lane, C.L, C.minD, mq);
         if (lane == 0) wrow[p0] = d;
     }
@@ -266,11 +277,14 @@ __global__ __launch_bounds__(256) void k_scan_line(float* __restrict__ vol,
     uint32_t mqorig = mq;
 #pragma unroll
     for (int j = 0; j < J; ++j) qorig[j] = q[j];
+    // omp emulation: next chunk start (INT_MAX when off)
+    int ct = 1;
+    int cs = (T > 1 && n > 0) ? omp_start(1, n, T) : 0x7fffffff;
 
     StepIn<J> ring[SC_K];
 #pragma unroll
     for (int k = 0; k < SC_K; ++k)
-        if (k < n) scan_issue<J, HORIZ>(ring[k], k, len, dir, line, base, es, gown, goth, im, mask, sgn, lane, C);
+        if (k < n) scan_issue<J, HORIZ, MASK>(ring[k], posbase + dir * k, dir, line, la, gown, goth, im, sgn, C);
 
     for (int b = 0; b < n; b += SC_K) {
 #pragma unroll
@@ -279,20 +293,23 @@ __global__ __launch_bounds__(256) void k_scan_line(float* __restrict__ vol,
             if (it < n) {
                 StepIn<J> s = ring[k];
                 if (it + SC_K < n)
-                    scan_issue<J, HORIZ>(ring[k], it + SC_K, len, dir, line, base, es, gown, goth, im, mask, sgn, lane, C);
+                    scan_issue<J, HORIZ, MASK>(ring[k], posbase + dir * (it + SC_K), dir, line, la, gown, goth,
+                                               im, sgn, C);
                 const int pos = posbase + dir * it;
                 const uint32_t sh = (uint32_t)((HORIZ ? x0a + pos : x0a) & 3);
-                if (T > 1 && omp_chunk_start(it, n, T)) {  // stale predecessor (racy schedule)
+                if (it == cs) {  // chunk start of the racy schedule: stale predecessor
 #pragma unroll
                     for (int j = 0; j < J; ++j) q[j] = qorig[j];
                     mq = mqorig;
+                    ++ct;
+                    cs = ct < T ? omp_start(ct, n, T) : 0x7fffffff;
                 }
-                if (T > 1 && omp_chunk_start(it + 1, n, T)) {
+                if (it + 1 == cs) {  // the next chunk's first pixel sees this pre-pass vector
 #pragma unroll
                     for (int j = 0; j < J; ++j) qorig[j] = s.p[j];
                     mqorig = vec_min_bits<J>(s.p);
                 }
-                const bool masked = mask && s.mk == 0;  // :824, :862
+                const bool masked = MASK && s.mk == 0;  // :824, :862
                 if (!(masked || mq == 0u)) {            // :880-881 -- else p stays untouched
                     partial_opt<J>(s.p, q, mq, s.d1, s, sh, rev, lane, C);
                     if (store) {
@@ -306,7 +323,7 @@ __global__ __launch_bounds__(256) void k_scan_line(float* __restrict__ vol,
 #pragma unroll
                 for (int j = 0; j < J; ++j) q[j] = s.p[j];
                 mq = vec_min_bits<J>(q);
-                if (wrow) {
+                if (WTA) {
                     const int d = vec_argmin<J>(q, lane, C.L, C.minD, mq);
                     if (lane == 0) wrow[pos] = d;
                 }
@@ -315,28 +332,42 @@ __global__ __launch_bounds__(256) void k_scan_line(float* __restrict__ vol,
     }
 }
 
-template <bool HORIZ>
-static int launch_scan(float* vol, const uint8_t* grad, const uint32_t* img, int dir, int32_t* wta,
-                       int store_view1, const DevParams& P, hipStream_t st) {
-    const int J = (P.Lp / 4 + 63) / 64;
+template <int J, bool HORIZ, bool MASK, bool WTA>
+static void launch_scan_t(float* vol, const uint8_t* grad, const uint32_t* img, int dir, int32_t* wta,
+                          int store_view1, const float* infvec, const DevParams& P, hipStream_t st) {
     dim3 g(((HORIZ ? P.H : P.W) + 3) / 4, 2);
-    switch (J) {
-        case 1: hipLaunchKernelGGL((k_scan_line<1, HORIZ>), g, dim3(256), 0, st, vol, grad, img, dir, wta, store_view1, P); break;
-        case 2: hipLaunchKernelGGL((k_scan_line<2, HORIZ>), g, dim3(256), 0, st, vol, grad, img, dir, wta, store_view1, P); break;
-        default: return -1;
+    hipLaunchKernelGGL((k_scan_line<J, HORIZ, MASK, WTA>), g, dim3(256), 0, st, vol, grad, img, dir, wta,
+                       store_view1, infvec, P);
+}
+
+template <bool HORIZ, bool WTA>
+static int launch_scan(float* vol, const uint8_t* grad, const uint32_t* img, int dir, int32_t* wta,
+                       int store_view1, const float* infvec, const DevParams& P, hipStream_t st) {
+    const int J = (P.Lp / 4 + 63) / 64;
+    const bool m = P.mask != 0;
+    if (J == 1) {
+        if (m) launch_scan_t<1, HORIZ, true, WTA>(vol, grad, img, dir, wta, store_view1, infvec, P, st);
+        else launch_scan_t<1, HORIZ, false, WTA>(vol, grad, img, dir, wta, store_view1, infvec, P, st);
+    } else if (J == 2) {
+        if (m) launch_scan_t<2, HORIZ, true, WTA>(vol, grad, img, dir, wta, store_view1, infvec, P, st);
+        else launch_scan_t<2, HORIZ, false, WTA>(vol, grad, img, dir, wta, store_view1, infvec, P, st);
+    } else {
+        return -1;
     }
     trace_point(HORIZ ? "k_scan_line<H>" : "k_scan_line<V>", st);
     return 0;
 }
 
 int launch_scan_vertical(float* vol, const uint8_t* gv, const uint32_t* img, int dir,
-                         const DevParams& P, hipStream_t st) {
-    return launch_scan<false>(vol, gv, img, dir, nullptr, 1, P, st);
+                         const float* infvec, const DevParams& P, hipStream_t st) {
+    return launch_scan<false, false>(vol, gv, img, dir, nullptr, 1, infvec, P, st);
 }
 
 int launch_scan_horizontal(float* vol, const uint8_t* gh, const uint32_t* img, int dir,
-                           int32_t* wta, int store_view1, const DevParams& P, hipStream_t st) {
-    return launch_scan<true>(vol, gh, img, dir, wta, store_view1, P, st);
+                           int32_t* wta, int store_view1, const float* infvec, const DevParams& P,
+                           hipStream_t st) {
+    if (wta) return launch_scan<true, true>(vol, gh, img, dir, wta, store_view1, infvec, P, st);
+    return launch_scan<true, false>(vol, gh, img, dir, nullptr, store_view1, infvec, P, st);
 }
 
 }  // namespace tsm

@@ -35,10 +35,12 @@ int launch_agg_line(float* vol, const uint32_t* arms, const int32_t* ws, int hor
                     const DevParams& P, hipStream_t st);
 
 // k_scanline.hip
+// infvec: >= 16 bytes of +inf (the vector lanes past the label axis read)
 int launch_scan_vertical(float* vol, const uint8_t* gv, const uint32_t* img, int dir,
-                         const DevParams& P, hipStream_t st);
+                         const float* infvec, const DevParams& P, hipStream_t st);
 int launch_scan_horizontal(float* vol, const uint8_t* gh, const uint32_t* img, int dir,
-                           int32_t* wta, int store_view1, const DevParams& P, hipStream_t st);
+                           int32_t* wta, int store_view1, const float* infvec, const DevParams& P,
+                           hipStream_t st);
 
 // k_refine.hip
 struct RefineBufs {
