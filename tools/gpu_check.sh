@@ -32,6 +32,10 @@ for s in "$@"; do
         pmc-cost-lds) step pmc_cost_lds 600 rocprofv3 --pmc SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_INSTS_LDS SQ_INSTS_VMEM_WR SQ_INSTS_VMEM_RD SQ_ACTIVE_INST_LDS SQ_INSTS_SALU SQ_WAVES --kernel-include-regex cost_walk --output-format csv -d gpurun_out/pmc_cost_lds -o run -- python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline --batch 2 --concurrency 1 ;;
         pmc-cost-write) step pmc_cost_write 600 rocprofv3 --pmc WRITE_SIZE --kernel-include-regex cost_walk --output-format csv -d gpurun_out/pmc_cost_write -o run -- python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline --batch 2 --concurrency 1 ;;
         pmc-cost-fetch) step pmc_cost_fetch 600 rocprofv3 --pmc FETCH_SIZE --kernel-include-regex cost_walk --output-format csv -d gpurun_out/pmc_cost_fetch -o run -- python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline --batch 2 --concurrency 1 ;;
+        pmc-cost) cd /tmp && export TMPDIR=/tmp && cd "$OLDPWD"
+              step pmc_cost_fetch 600 rocprofv3 --pmc FETCH_SIZE --kernel-include-regex cost_walk --output-format csv -d gpurun_out/pmc_cost_fetch -o run -- python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline --batch 2 --concurrency 1
+              step pmc_cost_write 600 rocprofv3 --pmc WRITE_SIZE --kernel-include-regex cost_walk --output-format csv -d gpurun_out/pmc_cost_write -o run -- python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline --batch 2 --concurrency 1
+              python3 tools/pmc_cost_json.py gpurun_out/pmc_cost_fetch/run_counter_collection.csv gpurun_out/pmc_cost_write/run_counter_collection.csv gpurun_out/cost_pmc.json ;;
         *) echo "unknown step $s"; exit 2 ;;
     esac
 done
