@@ -266,7 +266,7 @@ __global__ __launch_bounds__(AG_THREADS) void k_agg_line(float* __restrict__ vol
 }
 
 // ---------------------------------------------------------------------------
-// 1-D aggregation v3: LDS-DMA line streamer (1 loader wave + 12 summing waves)
+// 1-D aggregation v3: LDS-DMA line streamer (4 loader waves + 12 summing waves)
 // ---------------------------------------------------------------------------
 // The pass is bound by how many bytes each CU keeps in flight, not by arithmetic.
 // A workgroup owns one line; the line's pixel vectors stream into an LDS ring in chunks
@@ -280,7 +280,7 @@ __global__ __launch_bounds__(AG_THREADS) void k_agg_line(float* __restrict__ vol
 // reference (lanes own float4 of labels).  In place: an output overwrites pixel p only
 // after the chunk holding p was staged, and later windows read p from the ring.
 constexpr int AGD_SUM_WAVES = 12;
-constexpr int AGD_LOAD_WAVES = 1;               // DMA issue is slow per wave: spread it
+constexpr int AGD_LOAD_WAVES = 4;               // DMA issue is slow per wave: spread it
 constexpr int AGD_OPW = 1;                      // outputs per summing wave per step
 constexpr int AGD_SEG = AGD_SUM_WAVES * AGD_OPW;  // pixels per chunk = outputs per step
 constexpr int AGD_THREADS = (AGD_SUM_WAVES + AGD_LOAD_WAVES) * 64;
@@ -338,21 +338,19 @@ __global__ __launch_bounds__(AGD_THREADS) void k_agg_dma(float* __restrict__ vol
     const int nchunks = (n + AGD_SEG - 1) / AGD_SEG;
     const bool loader = wave >= AGD_SUM_WAVES;
     const int li = wave - AGD_SUM_WAVES;            // loader index (valid when loader)
-    // this loader's DMA instructions of a chunk: k = li, li + NLOAD, ... < ndma
-    const int nmine = loader ? (ndma - li + AGD_LOAD_WAVES - 1) / AGD_LOAD_WAVES : 0;
 
-    // loader: DMA chunk c (pixels c*SEG ..) into ring slot c % RC; the ring is pixel-
-    // linear (pixel p at (p mod RC*SEG) * Q).  Instruction k moves chunk float4
-    // f = 64 k + lane (pixel f / Q, group f % Q); the last one runs with only the lanes
-    // that still hold chunk data active, so no DMA writes outside its chunk.  Pixels
-    // past the line end re-read a valid vector into slots nobody reads.  Per-lane
-    // offsets are computed once (no per-step divisions).
-    constexpr int KMAX = (AGD_SEG * J + AGD_LOAD_WAVES - 1) / AGD_LOAD_WAVES;  // per loader
+    // Loaders take whole chunks in turn (chunk c: loader c % NLOAD), so each has NLOAD
+    // steps to issue a chunk's DMAs (their issue is slow per wave).  Chunk c goes to
+    // ring slot c % RC; the ring is pixel-linear (pixel p at (p mod RC*SEG) * Q).
+    // Instruction k moves chunk float4 f = 64 k + lane (pixel f / Q, group f % Q); the
+    // last one runs with only the lanes that still hold chunk data, so no DMA writes
+    // outside its chunk.  Pixels past the line end re-read a valid vector into slots
+    // nobody reads.  Per-lane offsets are computed once (no per-step divisions).
+    constexpr int KMAX = AGD_SEG * J;  // ndma <= SEG * ceil(Q / 64)
     int pxo[KMAX];
     uint32_t gofs[KMAX];
 #pragma unroll
-    for (int m = 0; m < KMAX; ++m) {
-        const int k = li + AGD_LOAD_WAVES * m;
+    for (int k = 0; k < KMAX; ++k) {
         const int f = k * 64 + lane;
         const bool data = f < AGD_SEG * Q;
         pxo[k] = data ? f / Q : 0;
@@ -360,18 +358,21 @@ __global__ __launch_bounds__(AGD_THREADS) void k_agg_dma(float* __restrict__ vol
     }
     const bool last_lane_ok = (ndma - 1) * 64 + lane < CS;
     auto dma_chunk = [&](int c) {
+        if (c % AGD_LOAD_WAVES != li) return;
         f32x4* slot = ring + (size_t)(c % RC) * CS;
 #pragma unroll
-        for (int m = 0; m < KMAX; ++m) {
-            const int k = li + AGD_LOAD_WAVES * m;
-            if (m < nmine && (k < ndma - 1 || last_lane_ok)) {
-                int px = c * AGD_SEG + pxo[m];
+        for (int k = 0; k < KMAX; ++k) {
+            if (k < ndma && (k < ndma - 1 || last_lane_ok)) {
+                int px = c * AGD_SEG + pxo[k];
                 px = px < n ? px : n - 1;
-                const float* src = base + (size_t)px * es + gofs[m];
+                const float* src = base + (size_t)px * es + gofs[k];
                 __builtin_amdgcn_global_load_lds(src, slot + k * 64, 16, 0, 0);
             }
         }
     };
+    // D - 1 is a multiple of NLOAD (host side), so after chunk s+AH every loader has
+    // issued exactly (D-1)/NLOAD younger chunks when step s begins
+    const int younger = ndma * ((D - 1) / AGD_LOAD_WAVES);
     if (loader) {
         for (int c = 0; c < AH + D; ++c) dma_chunk(c);  // chunks past the end: dead slots
     }
@@ -389,7 +390,7 @@ __global__ __launch_bounds__(AGD_THREADS) void k_agg_dma(float* __restrict__ vol
 #endif
     for (int s = 0; s < nchunks; ++s) {
         AGS(ta);
-        if (loader) wait_vmcnt((D - 1) * nmine);  // my part of chunk s+AH landed (D-1 younger chunks fly)
+        if (loader) wait_vmcnt(younger);  // chunk s+AH landed (younger chunks stay in flight)
         AGS(tb);
         // bare s_barrier, NOT __syncthreads(): its fence would drain every wave's vmcnt,
         // i.e. wait for all DMAs in flight and serialise the stream.  Summing waves
@@ -515,7 +516,9 @@ static size_t agg_dma_geometry(const DevParams& P, int& RC, int& D) {
     }();
     if (dcap >= 2 && rc > 2 * AH + 1 + dcap) rc = 2 * AH + 1 + dcap;
     D = rc - (2 * AH + 1);
+    D -= (D - 1) % AGD_LOAD_WAVES;  // D - 1 a multiple of the loader count
     if (D < 2) return 0;
+    rc = 2 * AH + 1 + D;
     RC = rc;
     return (size_t)rc * chunk + fixed;
 }
