@@ -303,7 +303,7 @@ __device__ __forceinline__ void wait_vmcnt(int n) {
 }
 
 #ifdef TSM_EXP_STAMPS
-__device__ unsigned long long g_agg_stamps[8192 * 9 * 4];  // [block][wave][total, vmwait, barrier, work]
+__device__ unsigned long long g_agg_stamps[8192 * 16 * 4];  // [block][wave][total, vmwait, barrier, work]
 #endif
 
 template <int J>
@@ -466,7 +466,7 @@ __global__ __launch_bounds__(AGD_THREADS) void k_agg_dma(float* __restrict__ vol
     {
         const size_t bid = (size_t)blockIdx.y * gridDim.x + blockIdx.x;
         if (lane == 0 && bid < 8192) {
-            unsigned long long* o = g_agg_stamps + (bid * 9 + wave) * 4;
+            unsigned long long* o = g_agg_stamps + (bid * 16 + wave) * 4;
             o[0] = __builtin_amdgcn_s_memtime() - t_start; o[1] = t_vm; o[2] = t_bar; o[3] = t_work;
         }
     }

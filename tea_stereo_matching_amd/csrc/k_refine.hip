@@ -207,10 +207,21 @@ __global__ __launch_bounds__(VD_THREADS) void k_vote_decide(
             const int yy0 = hf ? y + o : y, xx0 = hf ? x : x + o;
             int a1, b1, a2, b2;
             region_arms(arms[(size_t)yy0 * W + xx0], hf, a1, b1, a2, b2);
-            for (int i = -a2; i <= b2; ++i) {
-                const int yy = hf ? y + o : y + i;
-                const int xx = hf ? x + i : x + o;
-                const int dv = disp[(size_t)yy * W + xx];
+            // four loads in flight before their histogram adds (the loads are L2 hits on a
+            // dependent chain otherwise); the bins are added in the same order
+            const ptrdiff_t st = hf ? 1 : W;
+            const int32_t* rp = disp + (size_t)yy0 * W + xx0;
+            int i = -a2;
+            for (; i + 3 <= b2; i += 4) {
+                const int d0 = rp[(ptrdiff_t)i * st], d1 = rp[(ptrdiff_t)(i + 1) * st];
+                const int d2 = rp[(ptrdiff_t)(i + 2) * st], d3 = rp[(ptrdiff_t)(i + 3) * st];
+                if (d0 >= minD) atomicAdd(&hist[d0 - minD], 1);
+                if (d1 >= minD) atomicAdd(&hist[d1 - minD], 1);
+                if (d2 >= minD) atomicAdd(&hist[d2 - minD], 1);
+                if (d3 >= minD) atomicAdd(&hist[d3 - minD], 1);
+            }
+            for (; i <= b2; ++i) {
+                const int dv = rp[(ptrdiff_t)i * st];
                 if (dv >= minD) atomicAdd(&hist[dv - minD], 1);
             }
         }
@@ -221,7 +232,15 @@ __global__ __launch_bounds__(VD_THREADS) void k_vote_decide(
             const int qp = out_list[k];
             const int c = vote[qp];
             const uint16_t* s = samples + (size_t)qp * kMaxSamples;
-            for (int m = 0; m < c; ++m) atomicAdd(&hist[s[m]], 1);
+            int m = 0;
+            for (; m + 3 < c; m += 4) {
+                const int s0 = s[m], s1 = s[m + 1], s2 = s[m + 2], s3 = s[m + 3];
+                atomicAdd(&hist[s0], 1);
+                atomicAdd(&hist[s1], 1);
+                atomicAdd(&hist[s2], 1);
+                atomicAdd(&hist[s3], 1);
+            }
+            for (; m < c; ++m) atomicAdd(&hist[s[m]], 1);
         }
         __builtin_amdgcn_wave_barrier();
         __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");

@@ -19,14 +19,14 @@ m.setMinMaxDisparity(0, D)
 for _ in range(2):
     m.compute(l, r)
 lib = _native.load()
-n = 8192 * 9 * 4
+n = 8192 * 16 * 4
 buf = np.zeros(n, dtype=np.uint64)
 lib.tsm_exp_agg_stamps(ctypes.c_void_p(buf.ctypes.data), ctypes.c_size_t(n * 8))
-st = buf.reshape(8192, 9, 4).astype(np.float64)
+st = buf.reshape(8192, 16, 4).astype(np.float64)
 nb = 2 * W  # last pass of the pipeline: vertical (hf=F on iteration 4 -> vertical second)
 used = st[:, :, 0].sum(axis=1) > 0
 st = st[used]
 print("blocks", st.shape[0])
-for w, name in ((0, "summing wave 0"), (7, "summing wave 7"), (8, "loader")):
+for w, name in ((0, "summing wave 0"), (11, "summing wave 11"), (12, "loader 0"), (15, "loader 3")):
     a = st[:, w, :]
     print(f"{name:15s} total {a[:,0].mean():9.0f}  vmwait {a[:,1].mean():9.0f}  barrier {a[:,2].mean():9.0f}  work {a[:,3].mean():9.0f}")
