@@ -455,13 +455,35 @@ int run_pipeline(tsm_adc* h, Workspace* w, const uint8_t* d_left, const uint8_t*
     }
     // --- aggregation: iterations x (1-D pass, 1-D pass + divide) -----------------------
     {
-        bool hf = true;  // costAggregate :776-782
+        // costAggregate :776-782: iteration it runs (first orientation, no divide) then
+        // (other orientation, divide by ws[hf]); hf alternates T,F,T,F.  Consecutive
+        // same-direction passes (2nd of an iteration + 1st of the next) run fused.
+        struct Pass { int horizontal; const int32_t* ws; };
+        std::vector<Pass> passes;
+        bool hf = true;
         for (int it = 0; it < h->params.iterations; ++it) {
             const int32_t* wsel = w->ws + (hf ? 0 : N);  // ws[v][hf?0:1] via the per-view stride 2N
-            if (launch_agg_line(w->vol, w->arms, nullptr, hf ? 1 : 0, P, st) != 0 ||
-                launch_agg_line(w->vol, w->arms, wsel, hf ? 0 : 1, P, st) != 0)
-                return fail(h, TSM_ERR_UNSUPPORTED, "aggregation: label count");
+            passes.push_back({hf ? 1 : 0, nullptr});
+            passes.push_back({hf ? 0 : 1, wsel});
             hf = !hf;
+        }
+        static const bool legacy = [] {
+            const char* e = getenv("TSM_AGG_KERNEL");  // tuning override: "line"/"dma" = v2/v3
+            return e && (e[0] == 'l' || e[0] == 'd');
+        }();
+        for (size_t i = 0; i < passes.size(); ++i) {
+            const Pass& a = passes[i];
+            int rcp;
+            if (legacy) {
+                rcp = launch_agg_line(w->vol, w->arms, a.ws, a.horizontal, P, st);
+            } else if (i + 1 < passes.size() && a.ws && !passes[i + 1].ws &&
+                       passes[i + 1].horizontal == a.horizontal) {
+                rcp = launch_agg_pass(w->vol, w->arms, a.ws, a.horizontal, true, P, st);
+                ++i;
+            } else {
+                rcp = launch_agg_pass(w->vol, w->arms, a.ws, a.horizontal, false, P, st);
+            }
+            if (rcp != 0) return fail(h, TSM_ERR_UNSUPPORTED, "aggregation: label count");
         }
     }
     mark();
