@@ -467,9 +467,12 @@ int run_pipeline(tsm_adc* h, Workspace* w, const uint8_t* d_left, const uint8_t*
             passes.push_back({hf ? 0 : 1, wsel});
             hf = !hf;
         }
+        // v3 (full-vector DMA streamer, one pass per launch) is the default: on config B it
+        // beats v4 (label-grouped, fused pairs), which is issue-bound on its 4-output
+        // divergent windows.  TSM_AGG_KERNEL=grp selects v4, =line the register-staged v2.
         static const bool legacy = [] {
-            const char* e = getenv("TSM_AGG_KERNEL");  // tuning override: "line"/"dma" = v2/v3
-            return e && (e[0] == 'l' || e[0] == 'd');
+            const char* e = getenv("TSM_AGG_KERNEL");
+            return !(e && e[0] == 'g');
         }();
         for (size_t i = 0; i < passes.size(); ++i) {
             const Pass& a = passes[i];
