@@ -146,7 +146,10 @@ int fail(tsm_adc* h, int code, const std::string& msg) {
             return fail(h, TSM_ERR_DEVICE, std::string(#expr) + ": " + hipGetErrorString(e_)); \
     } while (0)
 
-int round_up4(int x) { return (x + 3) & ~3; }
+#ifndef TSM_EXP_LP_ALIGN
+#define TSM_EXP_LP_ALIGN 4
+#endif
+int round_up4(int x) { return (x + TSM_EXP_LP_ALIGN - 1) / TSM_EXP_LP_ALIGN * TSM_EXP_LP_ALIGN; }
 
 // Supported geometry: the aggregation LDS ring must fit 160 KiB and the per-line
 // kernels hold up to 4 float4 groups per lane.
@@ -467,25 +470,26 @@ int run_pipeline(tsm_adc* h, Workspace* w, const uint8_t* d_left, const uint8_t*
             passes.push_back({hf ? 0 : 1, wsel});
             hf = !hf;
         }
-        // v3 (full-vector DMA streamer, one pass per launch) is the default: on config B it
-        // beats v4 (label-grouped, fused pairs), which is issue-bound on its 4-output
-        // divergent windows.  TSM_AGG_KERNEL=grp selects v4, =line the register-staged v2.
-        static const bool legacy = [] {
+        // v5 (persistent line streamer, pairs fused) where the geometry fits; the v3 DMA
+        // streamer (one pass per launch) otherwise.  TSM_AGG_KERNEL=dma forces v3,
+        // =grp the label-grouped v4.
+        static const int kind = [] {
             const char* e = getenv("TSM_AGG_KERNEL");
-            return !(e && e[0] == 'g');
+            return !e ? 0 : e[0] == 'd' ? 1 : e[0] == 'g' ? 2 : 0;
         }();
         for (size_t i = 0; i < passes.size(); ++i) {
             const Pass& a = passes[i];
-            int rcp;
-            if (legacy) {
-                rcp = launch_agg_line(w->vol, w->arms, a.ws, a.horizontal, P, st);
-            } else if (i + 1 < passes.size() && a.ws && !passes[i + 1].ws &&
-                       passes[i + 1].horizontal == a.horizontal) {
-                rcp = launch_agg_pass(w->vol, w->arms, a.ws, a.horizontal, true, P, st);
-                ++i;
-            } else {
-                rcp = launch_agg_pass(w->vol, w->arms, a.ws, a.horizontal, false, P, st);
+            const bool pair = i + 1 < passes.size() && a.ws && !passes[i + 1].ws &&
+                              passes[i + 1].horizontal == a.horizontal;
+            int rcp = -1;
+            if (kind == 0) {
+                rcp = launch_agg_stream(w->vol, w->arms, a.ws, a.horizontal, pair, P, st);
+                if (rcp == 0 && pair) ++i;
+            } else if (kind == 2) {
+                rcp = launch_agg_pass(w->vol, w->arms, a.ws, a.horizontal, pair, P, st);
+                if (rcp == 0 && pair) ++i;
             }
+            if (rcp != 0) rcp = launch_agg_line(w->vol, w->arms, a.ws, a.horizontal, P, st);
             if (rcp != 0) return fail(h, TSM_ERR_UNSUPPORTED, "aggregation: label count");
         }
     }

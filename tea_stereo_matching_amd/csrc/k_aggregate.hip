@@ -453,7 +453,11 @@ __global__ __launch_bounds__(AGD_THREADS) void k_agg_dma(float* __restrict__ vol
 #pragma unroll
                 for (int j = 0; j < J; ++j) {
                     const int q = lane + 64 * j;
+#ifdef TSM_EXP_AGG_NOSTORE
+                    if (q < Q && acc[j].x == -1.f) *reinterpret_cast<f32x4*>(base + (size_t)o * es + 4 * q) = acc[j];
+#else
                     if (q < Q) *reinterpret_cast<f32x4*>(base + (size_t)o * es + 4 * q) = acc[j];
+#endif
                 }
             }
         }
@@ -643,6 +647,420 @@ __global__ __launch_bounds__(AGG_THREADS) void k_agg_grp(float* __restrict__ vol
     if (loader) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // no DMA outlives the WG
 }
 
+// ---------------------------------------------------------------------------
+// 1-D aggregation v5: persistent line streamer, same-direction pass pairs fused
+// ---------------------------------------------------------------------------
+// Each workgroup (one per CU) owns every G-th line of the pass (both views) and treats
+// them as ONE continuous pixel stream: windows never cross a line (arms stop at the
+// image border), so lines simply follow each other and there is no per-line warm-up.
+// The stream moves in chunks of AS_SEG pixels, one chunk per step.  Eight loader waves
+// stage chunk PAIRS in VGPRs (global_load_dwordx4; loader k % 8 owns pair k, one pair in
+// flight per loader = 16 chunks = ~100 KB per CU for config B) and copy a landed pair
+// into an LDS ring (ring1) AS_AHEAD steps before its first chunk is summed.  Each of the
+// AS_SEG summing waves produces one output per step with the reference's strictly
+// sequential window sum (lanes own float4 of labels).
+//   FUSED: pass A (the 2nd pass of an iteration, divided by the window sizes) writes
+//   its outputs to a second ring (ring2) and pass B (the 1st pass of the next
+//   iteration, same direction) sums them AS_LAG steps later, so the volume makes one
+//   HBM round trip for two passes.  Not fused: pass A's outputs go straight to HBM.
+// In place: a pixel is overwritten AS_AHEAD (+AS_LAG) steps after it was staged.
+// The per-pixel window sizes divide through an exact reciprocal-FMA quotient:
+// q0 = a*y, r = fma(-q0, b, a), q = fma(r, y, q0) with y = RN(1/b) equals RN(a/b) for
+// every integer b in [1, 4489] and every a in [2^-40, 2^16) (exhaustively checked,
+// tools/micro/div_check.c); smaller a take the IEEE division.
+constexpr int AS_SEG = 8;                   // pixels per chunk = summing waves
+constexpr int AS_LOAD = 8;                  // loader waves (pair k = chunks 2k, 2k+1: loader k % 8)
+constexpr int AS_THREADS = (AS_SEG + AS_LOAD) * 64;
+constexpr int AS_AH = 5;                    // windows reach at most 5 chunks either side
+constexpr int AS_MAX_ARM = AS_AH * AS_SEG;
+constexpr int AS_AHEAD = AS_AH + 1;         // chunk c is in ring1 from step c - AHEAD (even c)
+constexpr int AS_RC1 = 2 * AS_AH + 3;       // ring1 chunks: 2*AH+1 read + a pair landing
+constexpr int AS_RC2 = 2 * AS_AH + 2;       // ring2 chunks: 2*AH+1 read + one written
+constexpr int AS_RP1 = AS_RC1 * AS_SEG;
+constexpr int AS_RP2 = AS_RC2 * AS_SEG;
+constexpr int AS_LAG = AS_AH + 1;           // pass B at step s outputs chunk s - LAG
+constexpr int AS_MC = 16;                   // meta ring chunks (> AHEAD + 1 + LAG)
+static_assert(AS_AHEAD % 2 == 0, "pairs land on even steps");
+
+// exact a / b for the aggregation's "C /= windowSize" (see above)
+__device__ __forceinline__ f32x4 div_ws(f32x4 a, float b, float y) {
+    const f32x4 q0 = a * y;
+    const f32x4 r = __builtin_elementwise_fma(-q0, f32x4{b, b, b, b}, a);
+    f32x4 q = __builtin_elementwise_fma(r, f32x4{y, y, y, y}, q0);
+    // 0 < a < 2^-40 (never seen in practice) takes the IEEE path; a == 0 is exact above
+    const u32x4 ab = __builtin_bit_cast(u32x4, a) - 1u;
+    const uint32_t lim = 0x2b800000u - 1u;
+    if (__builtin_expect(ab.x < lim || ab.y < lim || ab.z < lim || ab.w < lim, 0)) {
+        q.x = a.x / b; q.y = a.y / b; q.z = a.z / b; q.w = a.w / b;
+    }
+    return q;
+}
+
+// raw buffer resource over p (gfx9 dword3: 32-bit data format, no swizzle); offsets are
+// unsigned 32-bit, the launcher checks that every line of a pass fits
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t make_rsrc(const void* p) {
+    return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p), (short)0, 0x7fffffff, 0x00020000);
+}
+
+struct AggStream {
+    float* vol;
+    const uint32_t* arms;
+    const int32_t* ws;     // window sizes of the dividing pass (nullptr: no divide)
+    int horizontal;
+    int n;                 // pixels per line
+    int cpl;               // chunks per line
+    int nlv;               // lines per view
+    int nl;                // lines of both views
+};
+
+#ifdef TSM_EXP_STAMPS
+__device__ unsigned long long g_as_stamps[1024 * 16 * 4];  // [block][wave][barrier, a/land, b/issue, total]
+#define AST_T(x) const unsigned long long x = __builtin_amdgcn_s_memtime()
+#define AST_ADD(i, v) ast[i] += (v)
+#define AST_FLUSH() do { if (FUSED && lane == 0 && blockIdx.x < 1024) { unsigned long long* o_ = g_as_stamps + ((size_t)blockIdx.x * 16 + wave) * 4; \
+    o_[0] = ast[0]; o_[1] = ast[1]; o_[2] = ast[2]; o_[3] = __builtin_amdgcn_s_memtime() - ast_t0; } } while (0)
+#else
+#define AST_T(x)
+#define AST_ADD(i, v)
+#define AST_FLUSH()
+#endif
+
+// Per-pixel window descriptor, precomputed by the loader when the pixel lands (so the
+// summing waves spend no scalar work on ring arithmetic): 32 B per pixel.
+//   [0] LDS byte offset of the pass-A window start in ring1   [1] window length
+//   [2] y = RN(1/windowSize)                                   [3] windowSize as float
+//   [4] LDS byte offset of the pass-B window start in ring2   [5] window length
+constexpr int AS_MW = 8;  // meta words per pixel
+
+// QT > 0: the pixel vector has QT float4 (compile-time ring stride); 0: runtime Q.
+template <bool FUSED, int QT>
+__global__ __launch_bounds__(AS_THREADS) void k_agg_stream(AggStream S, DevParams Pk) {
+    const DevParams P = Pk;
+    extern __shared__ __attribute__((aligned(16))) f32x4 smem_f4[];
+    const int H = P.H, W = P.W, Lp = P.Lp;
+    const int Q = QT > 0 ? QT : Lp >> 2;
+    const uint32_t Qs = (uint32_t)Q * 16;                                // bytes per ring pixel
+    const size_t vstride = (size_t)H * W * Lp;
+    const size_t es = S.horizontal ? (size_t)Lp : (size_t)W * Lp;         // floats per pixel step
+    const size_t ls = S.horizontal ? (size_t)W * Lp : (size_t)Lp;          // floats per line step
+    const size_t aes = S.horizontal ? 1 : (size_t)W;
+    const size_t als = S.horizontal ? (size_t)W : 1;
+    const int shA = S.horizontal ? 16 : 0, shB = S.horizontal ? 24 : 8;
+    const int g = blockIdx.x, G = gridDim.x;
+    const int my_lines = (S.nl - g + G - 1) / G;
+    const int nch = my_lines * S.cpl;
+    const uint32_t r1_off = 0;                                            // LDS byte offsets
+    const uint32_t r2_off = (uint32_t)AS_RP1 * Qs;
+    const uint32_t meta_off = r2_off + (FUSED ? (uint32_t)AS_RP2 * Qs : 0u);
+    const uint32_t zero_off = meta_off + (uint32_t)AS_MC * AS_SEG * AS_MW * 4;
+    char* lds = reinterpret_cast<char*>(smem_f4);
+
+    const int tid = threadIdx.x;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int lane = tid & 63;
+    const bool loader = wave >= AS_SEG;
+    const int li = wave - AS_SEG;
+    const int nsteps = nch + (FUSED ? AS_LAG : 0);
+    const uint32_t lane16 = (uint32_t)lane * 16;
+    const bool vl = lane < Q;
+#ifdef TSM_EXP_STAMPS
+    unsigned long long ast[3] = {0, 0, 0};
+    const unsigned long long ast_t0 = __builtin_amdgcn_s_memtime();
+#endif
+    // float offset of pixel 0 of local line lidx
+    auto line_base = [&](int lidx) -> size_t {
+        const int gl = g + lidx * G;
+        const int v = gl / S.nlv, line = gl - v * S.nlv;
+        return (size_t)v * vstride + (size_t)line * ls;
+    };
+
+    if (loader) {
+        // ---- loader li: pairs k = li, li + 8, ... (chunks 2k, 2k+1), one pair in flight ----
+        // (one buffer per wave: the compiler's wait before the copy is a plain vmcnt(0))
+        // Every load and LDS write is unconditional (lanes past the vector repeat lane
+        // Q-1): with no exec branches the compiler's waits stay at the copy (land) and
+        // never stall the next pair's issue.
+        f32x4 b[2 * AS_SEG];
+        uint32_t ma[2] = {0, 0}, mw[2] = {0, 0};  // meta of chunk 2k+h (pixel lane & 7)
+        const int lanec = lane < Q ? lane : Q - 1;
+        int lidx = 0, cc = 2 * li;                 // stream position of chunk 2k
+        while (cc >= S.cpl) { cc -= S.cpl; ++lidx; }
+        // Byte offsets of the two lines a pair can touch (vol, arms, window sizes), rebuilt
+        // (one division) only when the pair moves to a new line.  Loads are buffer loads
+        // off kernel-wide resources: a shared lane offset (VGPR) plus a per-pixel scalar
+        // offset, so no 64-bit VGPR addresses compete with the staging buffer.
+        const __amdgpu_buffer_rsrc_t rs_vol = make_rsrc(S.vol), rs_arm = make_rsrc(S.arms),
+                                     rs_ws = make_rsrc(S.ws);
+        struct LineRes { int l; uint32_t vol, arm, ws; };
+        auto line_res = [&](int l) -> LineRes {
+            const int gl = g + l * G;
+            const int v = gl / S.nlv, line = gl - v * S.nlv;
+            const uint32_t a = (uint32_t)(v * H * W + line * (int)als);
+            return LineRes{l, (uint32_t)(((size_t)v * vstride + (size_t)line * ls) * 4), a * 4,
+                           (a + (uint32_t)(v * H * W)) * 4};  // ws: per-view stride 2HW
+        };
+        LineRes lr0 = line_res(0), lr1 = lr0;
+        const int last_l = my_lines - 1, last_cc = S.cpl - 1;
+        const uint32_t voff = (uint32_t)lanec * 16;
+        const uint32_t es4 = (uint32_t)(es * 4), aes4 = (uint32_t)(aes * 4);
+        const uint32_t mpx = (uint32_t)(lane & 7);
+        auto issue = [&]() {  // pair at (lidx, cc): chunk 2k and its successor
+            int l[2], c[2];
+            l[0] = lidx; c[0] = cc;
+            l[1] = cc + 1 == S.cpl ? lidx + 1 : lidx;
+            c[1] = cc + 1 == S.cpl ? 0 : cc + 1;
+#pragma unroll
+            for (int h = 0; h < 2; ++h)
+                if (l[h] > last_l) { l[h] = last_l; c[h] = last_cc; }  // past the end: re-read
+            if (lr0.l != l[0]) lr0 = lr1.l == l[0] ? lr1 : line_res(l[0]);
+            if (lr1.l != l[1]) lr1 = lr0.l == l[1] ? lr0 : line_res(l[1]);
+            // meta first: a wait the compiler places before a meta load then finds no
+            // vector load of this pair in flight yet
+#pragma unroll
+            for (int h = 0; h < 2; ++h) {  // every lane loads (pixel lane & 7): no exec branches
+                const LineRes& r = h ? lr1 : lr0;
+                const uint32_t pos = min((uint32_t)c[h] * AS_SEG + mpx, (uint32_t)S.n - 1);
+                ma[h] = (uint32_t)__builtin_amdgcn_raw_buffer_load_b32(rs_arm, pos * aes4, r.arm, 0);
+                mw[h] = S.ws ? (uint32_t)__builtin_amdgcn_raw_buffer_load_b32(rs_ws, pos * aes4, r.ws, 0) : 1u;
+            }
+#pragma unroll
+            for (int h = 0; h < 2; ++h) {
+                const LineRes& r = h ? lr1 : lr0;
+                const int p0 = c[h] * AS_SEG;
+#pragma unroll
+                for (int i = 0; i < AS_SEG; ++i) {
+                    const uint32_t pos = (uint32_t)min(p0 + i, S.n - 1);
+                    b[h * AS_SEG + i] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rs_vol, voff, r.vol + pos * es4, 0));
+                }
+            }
+        };
+        auto land = [&](int k) {
+#pragma unroll
+            for (int h = 0; h < 2; ++h) {
+                const int c = 2 * k + h;
+                char* slot = lds + r1_off + (uint32_t)(c % AS_RC1) * AS_SEG * Qs + (uint32_t)lanec * 16;
+#pragma unroll
+                for (int i = 0; i < AS_SEG; ++i) *reinterpret_cast<f32x4*>(slot + i * Qs) = b[h * AS_SEG + i];
+            }
+            if (lane < 2 * AS_SEG) {  // window descriptors of the pair's 16 pixels
+                const int c = 2 * k + (lane >> 3), px = lane & 7;
+                const uint32_t a = lane < AS_SEG ? ma[0] : ma[1];
+                const int lo = (a >> shA) & 0xff, hi = (a >> shB) & 0xff;
+                const float bw = (float)(int)(lane < AS_SEG ? mw[0] : mw[1]);
+                const int rp1 = (c % AS_RC1) * AS_SEG + px;
+                const int rp2 = (c % AS_RC2) * AS_SEG + px;
+                uint32_t* m = reinterpret_cast<uint32_t*>(lds + meta_off) + ((c % AS_MC) * AS_SEG + px) * AS_MW;
+                m[0] = r1_off + (uint32_t)((rp1 - lo + AS_RP1) % AS_RP1) * Qs;
+                m[1] = (uint32_t)(lo + hi + 1);
+                m[2] = __float_as_uint(1.0f / bw);
+                m[3] = __float_as_uint(bw);
+                m[4] = r2_off + (uint32_t)((rp2 - lo + AS_RP2) % AS_RP2) * Qs;
+                m[5] = (uint32_t)(lo + hi + 1);
+            }
+        };
+        auto advance = [&]() {  // to the loader's next pair: 2 * AS_LOAD chunks on
+            cc += 2 * AS_LOAD;
+            while (cc >= S.cpl) { cc -= S.cpl; ++lidx; }
+        };
+        // prologue: pair li in flight; pairs with chunks < AHEAD land before step 0
+        issue();
+        if (2 * li < AS_AHEAD) {
+            land(li);
+            advance();
+            issue();
+        }
+        asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+        for (int t = 0; t < nsteps; ++t) {
+            // pair k lands during step 2k - AHEAD
+            const int k = (t + AS_AHEAD) >> 1;
+            if (!(t & 1) && (k & (AS_LOAD - 1)) == li && 2 * k < nch) {
+                AST_T(t0);
+                land(k);
+                AST_T(t1);
+                advance();
+                issue();
+                AST_T(t2);
+                AST_ADD(1, t1 - t0);
+                AST_ADD(2, t2 - t1);
+            }
+            AST_T(b0);
+            asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+            AST_T(b1);
+            AST_ADD(0, b1 - b0);
+        }
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // no load outlives the workgroup
+        AST_FLUSH();
+        return;
+    }
+
+    // ---- summing waves -------------------------------------------------------------
+    // Sequential window sum of `len` ring pixels from LDS byte offset `off` in the ring
+    // [rb, re).  Whole blocks of 4 that do not wrap read at immediate offsets; the last
+    // (partial) block and wrapping blocks go pixel by pixel, slots past the window
+    // reading the zero vector (a scalar select): x + 0.0 == x for the non-negative sums.
+    auto window = [&](uint32_t off, int len, uint32_t rb, uint32_t re) -> f32x4 {
+        f32x4 acc = f32x4{0.f, 0.f, 0.f, 0.f};
+        const char* lp = lds + lane16;
+#ifdef TSM_EXP_AGG_W1
+        return *reinterpret_cast<const f32x4*>(lp + off);  // timing experiment only
+#endif
+        int j = 0;
+        for (; j + 4 <= len && off + 4 * Qs <= re; j += 4) {
+            const char* p = lp + off;
+            const f32x4 x0 = *reinterpret_cast<const f32x4*>(p);
+            const f32x4 x1 = *reinterpret_cast<const f32x4*>(p + Qs);
+            const f32x4 x2 = *reinterpret_cast<const f32x4*>(p + 2 * Qs);
+            const f32x4 x3 = *reinterpret_cast<const f32x4*>(p + 3 * Qs);
+            acc += x0;
+            acc += x1;
+            acc += x2;
+            acc += x3;
+            off += 4 * Qs;
+            off = off == re ? rb : off;
+        }
+        for (; j < len; j += 4) {
+            f32x4 x[4];
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                const uint32_t o = j + u < len ? off : zero_off;
+                x[u] = *reinterpret_cast<const f32x4*>(lp + o);
+                off += Qs;
+                off = off == re ? rb : off;
+            }
+#pragma unroll
+            for (int u = 0; u < 4; ++u) acc += x[u];
+        }
+        return acc;
+    };
+    // output position of chunk `c`'s pixel `wave`: running float offset, new line: one division
+    struct Out {
+        int lidx, cc;
+        size_t off;
+    };
+#ifdef TSM_EXP_AGG_NOSTORE
+    const bool st_ok = false;  // timing experiment only
+#else
+    const bool st_ok = true;
+#endif
+    auto out_init = [&](Out& o) { o.lidx = 0; o.cc = 0; o.off = line_base(0) + (size_t)wave * es; };
+    auto out_step = [&](Out& o) {
+        if (++o.cc == S.cpl) { o.cc = 0; ++o.lidx; if (o.lidx < my_lines) o.off = line_base(o.lidx) + (size_t)wave * es; }
+        else o.off += (size_t)AS_SEG * es;
+    };
+    if (wave == 0 && vl) *reinterpret_cast<f32x4*>(lds + zero_off + lane16) = f32x4{0.f, 0.f, 0.f, 0.f};
+    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");  // prologue chunks landed
+    Out oa, ob;
+    out_init(oa);
+    out_init(ob);
+    const uint32_t mstep = AS_SEG * AS_MW * 4, mwrap = AS_MC * mstep;
+    const uint32_t* mbase = reinterpret_cast<const uint32_t*>(lds + meta_off + (uint32_t)wave * AS_MW * 4);
+    uint32_t ma_off = 0;                                            // meta of chunk s (pass A)
+    uint32_t mb_off = (uint32_t)((AS_MC - AS_LAG) % AS_MC) * mstep; // meta of chunk s - LAG (pass B)
+    uint32_t r2w = r2_off + (uint32_t)wave * Qs;                   // ring2 slot of chunk s
+    // descriptors are read one step ahead (they landed AHEAD steps before use)
+    u32x4 mA = *reinterpret_cast<const u32x4*>(reinterpret_cast<const char*>(mbase) + ma_off);
+    uint2 mB = *reinterpret_cast<const uint2*>(reinterpret_cast<const char*>(mbase) + mb_off + 16);
+    for (int s = 0; s < nsteps; ++s) {
+        const uint32_t a_off = __builtin_amdgcn_readfirstlane(mA.x);
+        const int a_len = (int)__builtin_amdgcn_readfirstlane(mA.y);
+        const float a_y = __uint_as_float(__builtin_amdgcn_readfirstlane(mA.z));
+        const float a_b = __uint_as_float(__builtin_amdgcn_readfirstlane(mA.w));
+        const uint32_t b_off = __builtin_amdgcn_readfirstlane(mB.x);
+        const int b_len = (int)__builtin_amdgcn_readfirstlane(mB.y);
+        ma_off += mstep;
+        ma_off = ma_off >= mwrap ? ma_off - mwrap : ma_off;
+        mb_off += mstep;
+        mb_off = mb_off >= mwrap ? mb_off - mwrap : mb_off;
+        mA = *reinterpret_cast<const u32x4*>(reinterpret_cast<const char*>(mbase) + ma_off);
+        mB = *reinterpret_cast<const uint2*>(reinterpret_cast<const char*>(mbase) + mb_off + 16);
+        AST_T(ta0);
+        // pass B first: it reads ring2 slots pass A does not write this step, so pass A's
+        // ring1 reads can overlap it
+        if (FUSED && s >= AS_LAG) {  // pass B on chunk s - LAG
+            if (ob.cc * AS_SEG + wave < S.n) {
+                const f32x4 acc = window(b_off, b_len, r2_off, r2_off + (uint32_t)AS_RP2 * Qs);
+                if (vl && (st_ok || acc.x == -1.f)) *reinterpret_cast<f32x4*>(S.vol + ob.off + 4 * lane) = acc;
+            }
+            out_step(ob);
+        }
+        AST_T(ta1);
+        AST_ADD(2, ta1 - ta0);
+        if (s < nch) {  // pass A on chunk s
+            if (oa.cc * AS_SEG + wave < S.n) {
+                f32x4 acc = window(a_off, a_len, r1_off, r1_off + (uint32_t)AS_RP1 * Qs);
+                if (S.ws) acc = div_ws(acc, a_b, a_y);
+                if (FUSED) {
+                    if (vl) *reinterpret_cast<f32x4*>(lds + r2w + lane16) = acc;
+                } else if (vl && (st_ok || acc.x == -1.f)) {
+                    *reinterpret_cast<f32x4*>(S.vol + oa.off + 4 * lane) = acc;
+                }
+            }
+            out_step(oa);
+            r2w += AS_SEG * Qs;
+            r2w = r2w >= r2_off + (uint32_t)AS_RP2 * Qs ? r2w - (uint32_t)AS_RP2 * Qs : r2w;
+        }
+        AST_T(ta2);
+        AST_ADD(1, ta2 - ta1);
+        asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+        AST_T(ta3);
+        AST_ADD(0, ta3 - ta2);
+    }
+    AST_FLUSH();
+}
+
+static size_t agg_stream_lds(const DevParams& P, bool fused) {
+    const int Q = P.Lp / 4;
+    return ((size_t)AS_RP1 + (fused ? AS_RP2 : 0) + 1) * Q * 16 + (size_t)AS_MC * AS_SEG * AS_MW * 4;
+}
+
+template <bool FUSED>
+static void agg_stream_attrs() {
+    (void)hipFuncSetAttribute((const void*)k_agg_stream<FUSED, 0>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    (void)hipFuncSetAttribute((const void*)k_agg_stream<FUSED, 49>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+}
+
+// Returns -1 if the streamer does not support the geometry (caller falls back).
+int launch_agg_stream(float* vol, const uint32_t* arms, const int32_t* ws, int horizontal, bool fused,
+                      const DevParams& P, hipStream_t st) {
+    const int Q = P.Lp / 4;
+    if (Q > 64 || P.max_length1 - 1 > AS_MAX_ARM) return -1;
+    if ((size_t)2 * P.H * P.W * P.Lp * 4 >= ((size_t)1 << 31)) return -1;  // 32-bit buffer offsets
+    const size_t lds = agg_stream_lds(P, fused);
+    if (lds > 160 * 1024) return -1;
+    static bool attr_set = false;
+    if (!attr_set) {
+        agg_stream_attrs<false>();
+        agg_stream_attrs<true>();
+        attr_set = true;
+    }
+    AggStream S;
+    S.vol = vol;
+    S.arms = arms;
+    S.ws = ws;
+    S.horizontal = horizontal;
+    S.n = horizontal ? P.W : P.H;
+    S.cpl = (S.n + AS_SEG - 1) / AS_SEG;
+    S.nlv = horizontal ? P.H : P.W;
+    S.nl = 2 * S.nlv;
+    static const int ncu = [] {
+        int dev = 0, n = 0;
+        (void)hipGetDevice(&dev);
+        (void)hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev);
+        return n > 0 ? n : 256;
+    }();
+    const int G = S.nl < ncu ? S.nl : ncu;
+    const dim3 grid(G), block(AS_THREADS);
+    if (fused) {
+        if (Q == 49) hipLaunchKernelGGL((k_agg_stream<true, 49>), grid, block, lds, st, S, P);
+        else hipLaunchKernelGGL((k_agg_stream<true, 0>), grid, block, lds, st, S, P);
+    } else {
+        if (Q == 49) hipLaunchKernelGGL((k_agg_stream<false, 49>), grid, block, lds, st, S, P);
+        else hipLaunchKernelGGL((k_agg_stream<false, 0>), grid, block, lds, st, S, P);
+    }
+    trace_point(fused ? "k_agg_stream<fused>" : "k_agg_stream", st);
+    return 0;
+}
+
 // Ring geometry of the grouped streamer: LDS bytes, ring1 chunks RC1 and DMA depth D
 // (D - 1 a multiple of the loader count), or 0 if it does not fit.
 static size_t agg_grp_geometry(const DevParams& P, bool fused, int& G, int& QG, int& RC1, int& D) {
@@ -781,6 +1199,9 @@ int launch_agg_line(float* vol, const uint32_t* arms, const int32_t* ws, int hor
 }  // namespace tsm
 
 #ifdef TSM_EXP_STAMPS
+extern "C" int tsm_exp_as_stamps(void* host, size_t bytes) {
+    return (int)hipMemcpyFromSymbol(host, HIP_SYMBOL(tsm::g_as_stamps), bytes, 0, hipMemcpyDeviceToHost);
+}
 extern "C" int tsm_exp_agg_stamps(void* host, size_t bytes) {
     return (int)hipMemcpyFromSymbol(host, HIP_SYMBOL(tsm::g_agg_stamps), bytes, 0, hipMemcpyDeviceToHost);
 }
