@@ -668,19 +668,22 @@ __global__ __launch_bounds__(AGG_THREADS) void k_agg_grp(float* __restrict__ vol
 // q0 = a*y, r = fma(-q0, b, a), q = fma(r, y, q0) with y = RN(1/b) equals RN(a/b) for
 // every integer b in [1, 4489] and every a in [2^-40, 2^16) (exhaustively checked,
 // tools/micro/div_check.c); smaller a take the IEEE division.
+#ifndef AS_GRP
+#define AS_GRP 1                            // chunks per loader turn
+#endif
 constexpr int AS_SEG = 8;                   // pixels per chunk = summing waves
-constexpr int AS_LOAD = 8;                  // loader waves (pair k = chunks 2k, 2k+1: loader k % 8)
+constexpr int AS_LOAD = 8;                  // loader waves (turn k: loader k % 8)
 constexpr int AS_THREADS = (AS_SEG + AS_LOAD) * 64;
 constexpr int AS_AH = 5;                    // windows reach at most 5 chunks either side
 constexpr int AS_MAX_ARM = AS_AH * AS_SEG;
-constexpr int AS_AHEAD = AS_AH + 1;         // chunk c is in ring1 from step c - AHEAD (even c)
-constexpr int AS_RC1 = 2 * AS_AH + 3;       // ring1 chunks: 2*AH+1 read + a pair landing
+constexpr int AS_AHEAD = AS_AH + 1;         // chunk c is readable from step c - AHEAD + 1
+constexpr int AS_RC1 = 2 * AS_AH + 1 + AS_GRP;  // ring1 chunks: 2*AH+1 read + a turn landing
 constexpr int AS_RC2 = 2 * AS_AH + 2;       // ring2 chunks: 2*AH+1 read + one written
 constexpr int AS_RP1 = AS_RC1 * AS_SEG;
 constexpr int AS_RP2 = AS_RC2 * AS_SEG;
 constexpr int AS_LAG = AS_AH + 1;           // pass B at step s outputs chunk s - LAG
-constexpr int AS_MC = 16;                   // meta ring chunks (> AHEAD + 1 + LAG)
-static_assert(AS_AHEAD % 2 == 0, "pairs land on even steps");
+constexpr int AS_MC = 16;                   // meta ring chunks (> AHEAD + GRP + LAG)
+static_assert(AS_AHEAD % AS_GRP == 0, "turns land on steps NG*k - AHEAD");
 
 // exact a / b for the aggregation's "C /= windowSize" (see above)
 __device__ __forceinline__ f32x4 div_ws(f32x4 a, float b, float y) {
@@ -775,18 +778,19 @@ __global__ __launch_bounds__(AS_THREADS) void k_agg_stream(AggStream S, DevParam
     };
 
     if (loader) {
-        // ---- loader li: pairs k = li, li + 8, ... (chunks 2k, 2k+1), one pair in flight ----
-        // (one buffer per wave: the compiler's wait before the copy is a plain vmcnt(0))
-        // Every load and LDS write is unconditional (lanes past the vector repeat lane
-        // Q-1): with no exec branches the compiler's waits stay at the copy (land) and
-        // never stall the next pair's issue.
-        f32x4 b[2 * AS_SEG];
-        uint32_t ma[2] = {0, 0}, mw[2] = {0, 0};  // meta of chunk 2k+h (pixel lane & 7)
+        // ---- loader li: turns k = li, li + 8, ... (chunks NG*k .. NG*k+NG-1), one turn's
+        // chunks in flight (one buffer per wave: the compiler's wait before the copy is a
+        // plain vmcnt(0)).  Every load and LDS write is unconditional (lanes past the
+        // vector repeat lane Q-1): with no exec branches the compiler's waits stay at the
+        // copy (land) and never stall the next turn's issue.
+        constexpr int NG = AS_GRP;
+        f32x4 b[NG * AS_SEG];
+        uint32_t ma[NG], mw[NG];                   // meta of chunk NG*k+h (pixel lane & 7)
         const int lanec = lane < Q ? lane : Q - 1;
-        int lidx = 0, cc = 2 * li;                 // stream position of chunk 2k
+        int lidx = 0, cc = NG * li;                // stream position of chunk NG*k
         while (cc >= S.cpl) { cc -= S.cpl; ++lidx; }
-        // Byte offsets of the two lines a pair can touch (vol, arms, window sizes), rebuilt
-        // (one division) only when the pair moves to a new line.  Loads are buffer loads
+        // Byte offsets of the lines a turn can touch (vol, arms, window sizes), rebuilt
+        // (one division) only when the turn moves to a new line.  Loads are buffer loads
         // off kernel-wide resources: a shared lane offset (VGPR) plus a per-pixel scalar
         // offset, so no 64-bit VGPR addresses compete with the staging buffer.
         const __amdgpu_buffer_rsrc_t rs_vol = make_rsrc(S.vol), rs_arm = make_rsrc(S.arms),
@@ -799,54 +803,60 @@ __global__ __launch_bounds__(AS_THREADS) void k_agg_stream(AggStream S, DevParam
             return LineRes{l, (uint32_t)(((size_t)v * vstride + (size_t)line * ls) * 4), a * 4,
                            (a + (uint32_t)(v * H * W)) * 4};  // ws: per-view stride 2HW
         };
-        LineRes lr0 = line_res(0), lr1 = lr0;
+        LineRes lr[NG];
+#pragma unroll
+        for (int h = 0; h < NG; ++h) lr[h] = line_res(0);
         const int last_l = my_lines - 1, last_cc = S.cpl - 1;
         const uint32_t voff = (uint32_t)lanec * 16;
         const uint32_t es4 = (uint32_t)(es * 4), aes4 = (uint32_t)(aes * 4);
         const uint32_t mpx = (uint32_t)(lane & 7);
-        auto issue = [&]() {  // pair at (lidx, cc): chunk 2k and its successor
-            int l[2], c[2];
+        auto issue = [&]() {  // the turn at (lidx, cc): chunk NG*k and its successors
+            int l[NG], c[NG];
             l[0] = lidx; c[0] = cc;
-            l[1] = cc + 1 == S.cpl ? lidx + 1 : lidx;
-            c[1] = cc + 1 == S.cpl ? 0 : cc + 1;
 #pragma unroll
-            for (int h = 0; h < 2; ++h)
-                if (l[h] > last_l) { l[h] = last_l; c[h] = last_cc; }  // past the end: re-read
-            if (lr0.l != l[0]) lr0 = lr1.l == l[0] ? lr1 : line_res(l[0]);
-            if (lr1.l != l[1]) lr1 = lr0.l == l[1] ? lr0 : line_res(l[1]);
-            // meta first: a wait the compiler places before a meta load then finds no
-            // vector load of this pair in flight yet
-#pragma unroll
-            for (int h = 0; h < 2; ++h) {  // every lane loads (pixel lane & 7): no exec branches
-                const LineRes& r = h ? lr1 : lr0;
-                const uint32_t pos = min((uint32_t)c[h] * AS_SEG + mpx, (uint32_t)S.n - 1);
-                ma[h] = (uint32_t)__builtin_amdgcn_raw_buffer_load_b32(rs_arm, pos * aes4, r.arm, 0);
-                mw[h] = S.ws ? (uint32_t)__builtin_amdgcn_raw_buffer_load_b32(rs_ws, pos * aes4, r.ws, 0) : 1u;
+            for (int h = 1; h < NG; ++h) {
+                l[h] = c[h - 1] + 1 == S.cpl ? l[h - 1] + 1 : l[h - 1];
+                c[h] = c[h - 1] + 1 == S.cpl ? 0 : c[h - 1] + 1;
             }
 #pragma unroll
-            for (int h = 0; h < 2; ++h) {
-                const LineRes& r = h ? lr1 : lr0;
+            for (int h = 0; h < NG; ++h) {
+                if (l[h] > last_l) { l[h] = last_l; c[h] = last_cc; }  // past the end: re-read
+                if (lr[h].l != l[h]) lr[h] = (h && lr[h - 1].l == l[h]) ? lr[h - 1] : line_res(l[h]);
+            }
+            // meta first: a wait the compiler places before a meta load then finds no
+            // vector load of this turn in flight yet
+#pragma unroll
+            for (int h = 0; h < NG; ++h) {  // every lane loads (pixel lane & 7): no exec branches
+                const uint32_t pos = min((uint32_t)c[h] * AS_SEG + mpx, (uint32_t)S.n - 1);
+                ma[h] = (uint32_t)__builtin_amdgcn_raw_buffer_load_b32(rs_arm, pos * aes4, lr[h].arm, 0);
+                mw[h] = S.ws ? (uint32_t)__builtin_amdgcn_raw_buffer_load_b32(rs_ws, pos * aes4, lr[h].ws, 0) : 1u;
+            }
+#pragma unroll
+            for (int h = 0; h < NG; ++h) {
                 const int p0 = c[h] * AS_SEG;
 #pragma unroll
                 for (int i = 0; i < AS_SEG; ++i) {
                     const uint32_t pos = (uint32_t)min(p0 + i, S.n - 1);
-                    b[h * AS_SEG + i] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rs_vol, voff, r.vol + pos * es4, 0));
+                    b[h * AS_SEG + i] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rs_vol, voff, lr[h].vol + pos * es4, 0));
                 }
             }
         };
         auto land = [&](int k) {
 #pragma unroll
-            for (int h = 0; h < 2; ++h) {
-                const int c = 2 * k + h;
+            for (int h = 0; h < NG; ++h) {
+                const int c = NG * k + h;
                 char* slot = lds + r1_off + (uint32_t)(c % AS_RC1) * AS_SEG * Qs + (uint32_t)lanec * 16;
 #pragma unroll
                 for (int i = 0; i < AS_SEG; ++i) *reinterpret_cast<f32x4*>(slot + i * Qs) = b[h * AS_SEG + i];
             }
-            if (lane < 2 * AS_SEG) {  // window descriptors of the pair's 16 pixels
-                const int c = 2 * k + (lane >> 3), px = lane & 7;
-                const uint32_t a = lane < AS_SEG ? ma[0] : ma[1];
+            if (lane < NG * AS_SEG) {  // window descriptors of the turn's pixels
+                const int hh = lane >> 3, c = NG * k + hh, px = lane & 7;
+                uint32_t a = ma[0], wsz = mw[0];
+#pragma unroll
+                for (int h = 1; h < NG; ++h)
+                    if (hh == h) { a = ma[h]; wsz = mw[h]; }
                 const int lo = (a >> shA) & 0xff, hi = (a >> shB) & 0xff;
-                const float bw = (float)(int)(lane < AS_SEG ? mw[0] : mw[1]);
+                const float bw = (float)(int)wsz;
                 const int rp1 = (c % AS_RC1) * AS_SEG + px;
                 const int rp2 = (c % AS_RC2) * AS_SEG + px;
                 uint32_t* m = reinterpret_cast<uint32_t*>(lds + meta_off) + ((c % AS_MC) * AS_SEG + px) * AS_MW;
@@ -858,22 +868,22 @@ __global__ __launch_bounds__(AS_THREADS) void k_agg_stream(AggStream S, DevParam
                 m[5] = (uint32_t)(lo + hi + 1);
             }
         };
-        auto advance = [&]() {  // to the loader's next pair: 2 * AS_LOAD chunks on
-            cc += 2 * AS_LOAD;
+        auto advance = [&]() {  // to the loader's next turn: NG * AS_LOAD chunks on
+            cc += NG * AS_LOAD;
             while (cc >= S.cpl) { cc -= S.cpl; ++lidx; }
         };
-        // prologue: pair li in flight; pairs with chunks < AHEAD land before step 0
+        // prologue: turn li in flight; turns with chunks < AHEAD land before step 0
         issue();
-        if (2 * li < AS_AHEAD) {
+        if (NG * li < AS_AHEAD) {
             land(li);
             advance();
             issue();
         }
         asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
         for (int t = 0; t < nsteps; ++t) {
-            // pair k lands during step 2k - AHEAD
-            const int k = (t + AS_AHEAD) >> 1;
-            if (!(t & 1) && (k & (AS_LOAD - 1)) == li && 2 * k < nch) {
+            // turn k lands during step NG*k - AHEAD
+            const int k = (t + AS_AHEAD) / NG;
+            if ((t + AS_AHEAD) % NG == 0 && (k & (AS_LOAD - 1)) == li && NG * k < nch) {
                 AST_T(t0);
                 land(k);
                 AST_T(t1);
@@ -974,11 +984,12 @@ __global__ __launch_bounds__(AS_THREADS) void k_agg_stream(AggStream S, DevParam
         mA = *reinterpret_cast<const u32x4*>(reinterpret_cast<const char*>(mbase) + ma_off);
         mB = *reinterpret_cast<const uint2*>(reinterpret_cast<const char*>(mbase) + mb_off + 16);
         AST_T(ta0);
+        const uint32_t r1_end = r1_off + (uint32_t)AS_RP1 * Qs, r2_end = r2_off + (uint32_t)AS_RP2 * Qs;
         // pass B first: it reads ring2 slots pass A does not write this step, so pass A's
         // ring1 reads can overlap it
         if (FUSED && s >= AS_LAG) {  // pass B on chunk s - LAG
             if (ob.cc * AS_SEG + wave < S.n) {
-                const f32x4 acc = window(b_off, b_len, r2_off, r2_off + (uint32_t)AS_RP2 * Qs);
+                const f32x4 acc = window(b_off, b_len, r2_off, r2_end);
                 if (vl && (st_ok || acc.x == -1.f)) *reinterpret_cast<f32x4*>(S.vol + ob.off + 4 * lane) = acc;
             }
             out_step(ob);
@@ -987,7 +998,7 @@ __global__ __launch_bounds__(AS_THREADS) void k_agg_stream(AggStream S, DevParam
         AST_ADD(2, ta1 - ta0);
         if (s < nch) {  // pass A on chunk s
             if (oa.cc * AS_SEG + wave < S.n) {
-                f32x4 acc = window(a_off, a_len, r1_off, r1_off + (uint32_t)AS_RP1 * Qs);
+                f32x4 acc = window(a_off, a_len, r1_off, r1_end);
                 if (S.ws) acc = div_ws(acc, a_b, a_y);
                 if (FUSED) {
                     if (vl) *reinterpret_cast<f32x4*>(lds + r2w + lane16) = acc;
@@ -997,7 +1008,7 @@ __global__ __launch_bounds__(AS_THREADS) void k_agg_stream(AggStream S, DevParam
             }
             out_step(oa);
             r2w += AS_SEG * Qs;
-            r2w = r2w >= r2_off + (uint32_t)AS_RP2 * Qs ? r2w - (uint32_t)AS_RP2 * Qs : r2w;
+            r2w = r2w >= r2_end ? r2w - (uint32_t)AS_RP2 * Qs : r2w;
         }
         AST_T(ta2);
         AST_ADD(1, ta2 - ta1);
