@@ -59,7 +59,7 @@ __device__ __forceinline__ uint32_t vec_min_bits(const f32x4 (&x)[J]) {
 #pragma unroll
     for (int j = 1; j < J; ++j)
         m = min(m, min(min(fbits(x[j][0]), fbits(x[j][1])), min(fbits(x[j][2]), fbits(x[j][3]))));
-    return __float_as_uint(wave_min_nonneg(bitsf(m)));
+    return wave_min_bits(m);
 }
 
 // WTA over indices [minD, L-1], first minimum (strict <, ADCensus.cpp:1404): the first d
@@ -75,7 +75,7 @@ __device__ __forceinline__ int vec_argmin(const f32x4 (&x)[J], int lane, int L, 
                 const int d = 4 * (lane + 64 * j) + e;
                 if (d >= minD) mm = min(mm, fbits(x[j][e]));
             }
-        m = __float_as_uint(wave_min_nonneg(bitsf(mm)));
+        m = wave_min_bits(mm);
     }
     if (!(bitsf(m) < 3.402823466e+38f)) return minD;  // nothing below FLT_MAX (reference: unset)
 #pragma unroll
@@ -119,13 +119,6 @@ struct StepIn {
     uint32_t mk;     // mask mode: predecessor's packed colour (0 = black)
 };
 
-// d2 bytes of this lane's 4 disparities from the 8-byte window: view 0 reads x ascending,
-// view 1 descending (x = pos -/+ (d + minD)), so view 1 byte-reverses.
-__device__ __forceinline__ uint32_t d2_bytes(uint32_t lo, uint32_t hi, uint32_t sh, bool rev) {
-    const uint32_t w = __builtin_amdgcn_alignbyte(hi, lo, sh);
-    return rev ? __builtin_amdgcn_perm(w, w, 0x00010203u) : w;
-}
-
 // Per-lane addressing, fixed for the whole walk: the vector element of lane q lives at
 // vbase + pos * ves (lanes >= Q: ves = 0 on a +inf vector, so no per-step select), its
 // d2 bytes at dbase + pos * dstep (8-byte aligned window, sentinel-padded map).
@@ -133,46 +126,62 @@ template <int J>
 struct LaneAddr {
     const float* vb[J];
     size_t ves[J];
-    int gb[J];  // byte offset of this lane's 4-byte d2 group relative to x0 (aligned later)
 };
 
+// Buffer resources of the byte maps / image; offsets are 32-bit (checked by the launcher).
+struct ScanRes {
+    __amdgpu_buffer_rsrc_t own;   // own-view colour differences (d1)
+    __amdgpu_buffer_rsrc_t oth;   // other view's colour differences (d2), based 256 B low
+    __amdgpu_buffer_rsrc_t im;    // own-view image (mask mode)
+};
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t scan_rsrc(const void* p) {
+    return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p), (short)0, 0x7fffffff, 0x00020000);
+}
+
+// Chain-independent loads of one step.  The pixel vector comes through the lane's running
+// pointer; d1, the mask colour and the d2 window are buffer loads whose offsets are
+// scalar (uniform) plus, for d2, a per-lane constant: no per-step address arithmetic.
+//   d2 window of lane q: aligned byte (x0 + gb) & ~3 = S + V with S = (x0 [- 3]) & ~3
+//   (scalar) and V = +4q (view 0) or -4q (view 1); the rsrc sits 256 B low so V + 256 >= 0.
 template <int J, bool HORIZ, bool MASK>
 __device__ __forceinline__ void scan_issue(StepIn<J>& s, int pos, int dir, int line,
-                                           const LaneAddr<J>& la, const uint8_t* gown,
-                                           const uint8_t* goth, const uint32_t* im,
-                                           int sgn, const ScanConst& C) {
+                                           const float* const (&pv)[J], const uint32_t (&gv)[J],
+                                           const ScanRes& R, uint32_t orow, int sgn,
+                                           const ScanConst& C) {
     const int pm = dir > 0 ? pos : pos + 1;  // max(pos, predecessor)
 #pragma unroll
-    for (int j = 0; j < J; ++j) s.p[j] = *reinterpret_cast<const f32x4*>(la.vb[j] + (size_t)pos * la.ves[j]);
-    // d1 / mask loads: wave-uniform addresses laundered into a VGPR, so they are
-    // vector loads ordered by vmcnt (a scalar load would need lgkmcnt(0) at its use)
-    int i1 = HORIZ ? C.gpad + pm : pm * C.gstride + C.gpad + line;
-    asm volatile("v_mov_b32 %0, %1" : "=v"(i1) : "v"(i1));
-    s.d1 = gown[i1];
+    for (int j = 0; j < J; ++j) s.p[j] = *reinterpret_cast<const f32x4*>(pv[j]);
+    const uint32_t i1 = (uint32_t)(HORIZ ? C.gpad + pm : pm * C.gstride + C.gpad + line);
+    s.d1 = (int)__builtin_amdgcn_raw_buffer_load_b8(R.own, 0u, orow + i1, 0);
     s.mk = 1u;
     if (MASK) {
-        int im_idx = HORIZ ? line * C.W + (pos - dir) : (pos - dir) * C.W + line;
-        asm volatile("v_mov_b32 %0, %1" : "=v"(im_idx) : "v"(im_idx));
-        s.mk = im[im_idx];
+        const uint32_t ii = (uint32_t)(HORIZ ? line * C.W + (pos - dir) : (pos - dir) * C.W + line);
+        s.mk = __builtin_amdgcn_raw_buffer_load_b32(R.im, 0u, ii * 4u, 0);
     }
     // x of lane 0's first disparity; HORIZ reads byte max(x1, x2) = x1 + (dir < 0)
-    const uint8_t* grow = HORIZ ? goth : goth + (size_t)pm * C.gstride;
     const int x0 = (HORIZ ? pos + (dir < 0 ? 1 : 0) : line) + C.gpad + sgn * C.minD;
+    const uint32_t so = (HORIZ ? orow : orow + (uint32_t)pm * C.gstride) +
+                        (uint32_t)((sgn > 0 ? x0 : x0 - 3) & ~3);
 #pragma unroll
     for (int j = 0; j < J; ++j) {
-        const uint2 w = *reinterpret_cast<const uint2*>(grow + ((x0 + la.gb[j]) & ~3));
+        const uint2 w = __builtin_bit_cast(uint2, __builtin_amdgcn_raw_buffer_load_b64(R.oth, gv[j], so, 0));
         s.g0[j] = w.x;
         s.g1[j] = w.y;
     }
 }
 
-// One partialOptimization step (ADCensus.cpp:869-913), branch-free.
+// One partialOptimization step (ADCensus.cpp:869-913), branch-free.  Everything that
+// is uniform over the step (d1's P1/P2 class, m + P2, the d2 byte selector) is scalar
+// work; per lane: one v_perm for the four d2 bytes, then per disparity two selects,
+// the neighbour adds (packed), an integer min3/min and the packed (C - m + min) / 2.
+//   psel: v_perm selector picking this step's 4 d2 bytes (in label order) out of the
+//   aligned 8-byte window
 template <int J>
 __device__ __forceinline__ void partial_opt(f32x4 (&p)[J], const f32x4 (&q)[J], uint32_t mq,
-                                            int d1, const StepIn<J>& s, uint32_t sh, bool rev,
+                                            int d1, const StepIn<J>& s, uint32_t psel,
                                             int lane, const ScanConst& C) {
     const float mqf = bitsf(mq);
-    // P1/P2 pairs by d1 class (:954-979): d2 similar -> a, dissimilar -> b
+    // P1/P2 pairs by d1 class (:954-979): d2 similar -> a, dissimilar -> b (scalar)
     const bool sim1 = d1 < C.cd;
     const float p1a = sim1 ? C.p1[2] : C.p1[1], p1b = sim1 ? C.p1[1] : C.p1[0];
     const float p2a = sim1 ? C.p2[2] : C.p2[1], p2b = sim1 ? C.p2[1] : C.p2[0];
@@ -192,7 +201,7 @@ __device__ __forceinline__ void partial_opt(f32x4 (&p)[J], const f32x4 (&q)[J], 
             const float nxt = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(q[j + 1][0]), 0));
             hi = lane == 63 ? nxt : hi;
         }
-        const uint32_t g = d2_bytes(s.g0[j], s.g1[j], sh, rev);
+        const uint32_t g = __builtin_amdgcn_perm(s.g1[j], s.g0[j], psel);
         const float qe[6] = {lo, q[j][0], q[j][1], q[j][2], q[j][3], hi};
         f32x4 pe = p[j];
 #pragma unroll
@@ -201,9 +210,10 @@ __device__ __forceinline__ void partial_opt(f32x4 (&p)[J], const f32x4 (&q)[J], 
             const float p1 = sim2 ? p1a : p1b;
             const float m2 = sim2 ? m2a : m2b;
             const float cost = pe[k] - mqf;
-            // min{ m + P2, C(q,d), C(q,d-1) + P1, C(q,d+1) + P1 } (all >= 0: integer min)
-            const uint32_t mo = umin3(min(fbits(m2), fbits(qe[k + 1])), fbits(qe[k] + p1),
-                                      fbits(qe[k + 2] + p1));
+            // min{ m + P2, C(q,d), C(q,d-1) + P1, C(q,d+1) + P1 }: rounding is monotonic,
+            // so min(a,b) + P1 == min(a + P1, b + P1) exactly (all >= 0: integer mins)
+            const float nb = bitsf(min(fbits(qe[k]), fbits(qe[k + 2])));
+            const uint32_t mo = umin3(fbits(m2), fbits(qe[k + 1]), fbits(nb + p1));
             pe[k] = (cost + bitsf(mo)) * 0.5f;  // == / 2 exactly
         }
         p[j] = pe;
@@ -217,7 +227,13 @@ __device__ __forceinline__ void partial_opt(f32x4 (&p)[J], const f32x4 (&q)[J], 
 // omp schedule emulation costs two scalar compares per step (chunk starts are tracked
 // incrementally).
 // ---------------------------------------------------------------------------
-constexpr int SC_K = 8;  // prefetch depth (steps)
+// Prefetch depth (steps).  The vertical passes run ~2.4 waves per SIMD over strided
+// columns and are HBM-bound at 8; the horizontal ones have under one wave per SIMD, so
+// each wave must keep more of its own row in flight.
+#ifndef TSM_SC_KH
+#define TSM_SC_KH 16
+#endif
+template <bool HORIZ> constexpr int sc_k() { return HORIZ ? TSM_SC_KH : 8; }
 
 // first iteration of omp-static chunk t (libgomp / vcomp: first n%T threads take q+1)
 __device__ __forceinline__ int omp_start(int t, int n, int T) {
@@ -225,7 +241,7 @@ __device__ __forceinline__ int omp_start(int t, int n, int T) {
     return t * q + (t < r ? t : r);
 }
 
-template <int J, bool HORIZ, bool MASK, bool WTA>
+template <int J, bool HORIZ, bool MASK, bool WTA, bool OMP>
 __global__ __launch_bounds__(256) void k_scan_line(float* __restrict__ vol,
                                                    const uint8_t* __restrict__ grad,
                                                    const uint32_t* __restrict__ img, int dir,
@@ -242,26 +258,32 @@ __global__ __launch_bounds__(256) void k_scan_line(float* __restrict__ vol,
     const int len = HORIZ ? W : H;
     const size_t es = HORIZ ? (size_t)Lp : (size_t)W * Lp;
     float* base = vol + (size_t)v * H * W * Lp + (HORIZ ? (size_t)line * W * Lp : (size_t)line * Lp);
-    const uint8_t* gown = grad + (size_t)v * H * C.gstride + (HORIZ ? (size_t)line * C.gstride : 0);
-    const uint8_t* goth = grad + (size_t)(1 - v) * H * C.gstride + (HORIZ ? (size_t)line * C.gstride : 0);
-    const uint32_t* im = img + (size_t)v * H * W;
     const int sgn = v == 0 ? 1 : -1;
+    ScanRes R;
+    R.own = scan_rsrc(grad + (size_t)v * H * C.gstride);
+    R.oth = scan_rsrc(grad + (size_t)(1 - v) * H * C.gstride - 256);
+    R.im = scan_rsrc(img + (size_t)v * H * W);
+    const uint32_t orow = HORIZ ? (uint32_t)line * (uint32_t)C.gstride : 0u;  // row offset in both maps
     const bool rev = sgn < 0;
     const int n = len - 1;
-    const int T = P.omp_threads;
+    const int T = OMP ? P.omp_threads : 1;
     const bool store = !(WTA && v == 1 && !store_view1);
     int32_t* wrow = WTA ? wta + ((size_t)v * H + line) * W : nullptr;
     // byte misalignment of every lane's d2 window (uniform: lanes differ by multiples of 4)
     const int x0a = (HORIZ ? (dir < 0 ? 1 : 0) : line) + C.gpad + sgn * C.minD - (sgn > 0 ? 0 : 3);
     const int posbase = dir > 0 ? 1 : len - 2;  // pos(it) = posbase + dir*it (HORIZ shifts x0)
+    // v_perm selector of the 4 d2 bytes at byte offset 0 of the (lo, hi) window: view 0
+    // reads x ascending, view 1 descending (byte-reversed); + sh * 0x01010101 per step
+    const uint32_t psel0 = rev ? 0x00010203u : 0x03020100u;
     LaneAddr<J> la;
+    uint32_t gv[J];  // d2 lane offsets (+256: the rsrc sits 256 B low)
 #pragma unroll
     for (int j = 0; j < J; ++j) {
         const int q = lane + 64 * j;
         const bool in = q < C.Q;
         la.vb[j] = in ? base + 4 * q : infvec;
         la.ves[j] = in ? es : 0;
-        la.gb[j] = in ? (sgn > 0 ? 4 * q : -4 * q - 3) : 0;
+        gv[j] = (uint32_t)(256 + (in ? (sgn > 0 ? 4 * q : -4 * q) : 0));
     }
 
     f32x4 q[J];
@@ -275,57 +297,93 @@ __global__ __launch_bounds__(256) void k_scan_line(float* __restrict__ vol,
     }
     f32x4 qorig[J];
     uint32_t mqorig = mq;
+    if (OMP) {
 #pragma unroll
-    for (int j = 0; j < J; ++j) qorig[j] = q[j];
+        for (int j = 0; j < J; ++j) qorig[j] = q[j];
+    }
     // omp emulation: next chunk start (INT_MAX when off)
     int ct = 1;
-    int cs = (T > 1 && n > 0) ? omp_start(1, n, T) : 0x7fffffff;
+    int cs = (OMP && T > 1 && n > 0) ? omp_start(1, n, T) : 0x7fffffff;
 
+    // running per-lane pointers: the prefetch position and the step being written
+    // (lanes past the label axis stay on the +inf vector: step 0; storing +inf there is a no-op)
+    constexpr int SC_K = sc_k<HORIZ>();
+    const float* pf[J];
+    float* cur[J];
+    ptrdiff_t dstep[J];
+#pragma unroll
+    for (int j = 0; j < J; ++j) {
+        dstep[j] = (ptrdiff_t)dir * (ptrdiff_t)la.ves[j];
+        cur[j] = const_cast<float*>(la.vb[j]) + (ptrdiff_t)posbase * (ptrdiff_t)la.ves[j];
+        pf[j] = cur[j];
+    }
     StepIn<J> ring[SC_K];
 #pragma unroll
-    for (int k = 0; k < SC_K; ++k)
-        if (k < n) scan_issue<J, HORIZ, MASK>(ring[k], posbase + dir * k, dir, line, la, gown, goth, im, sgn, C);
+    for (int k = 0; k < SC_K; ++k) {
+        const int kk = k < n ? k : n - 1;  // past the end: re-read the last pixel (unused)
+        scan_issue<J, HORIZ, MASK>(ring[k], posbase + dir * kk, dir, line, pf, gv, R, orow, sgn, C);
+        if (k + 1 < n) {
+#pragma unroll
+            for (int j = 0; j < J; ++j) pf[j] += dstep[j];
+        }
+    }
+    int pfi = SC_K < n ? SC_K : n - 1;  // step index pf points at (clamped to the last)
 
     for (int b = 0; b < n; b += SC_K) {
 #pragma unroll
         for (int k = 0; k < SC_K; ++k) {
             const int it = b + k;
             if (it < n) {
-                StepIn<J> s = ring[k];
-                if (it + SC_K < n)
-                    scan_issue<J, HORIZ, MASK>(ring[k], posbase + dir * (it + SC_K), dir, line, la, gown, goth,
-                                               im, sgn, C);
+                const StepIn<J>& s = ring[k];
                 const int pos = posbase + dir * it;
                 const uint32_t sh = (uint32_t)((HORIZ ? x0a + pos : x0a) & 3);
-                if (it == cs) {  // chunk start of the racy schedule: stale predecessor
+                if (OMP) {
+                    if (it == cs) {  // chunk start of the racy schedule: stale predecessor
 #pragma unroll
-                    for (int j = 0; j < J; ++j) q[j] = qorig[j];
-                    mq = mqorig;
-                    ++ct;
-                    cs = ct < T ? omp_start(ct, n, T) : 0x7fffffff;
-                }
-                if (it + 1 == cs) {  // the next chunk's first pixel sees this pre-pass vector
+                        for (int j = 0; j < J; ++j) q[j] = qorig[j];
+                        mq = mqorig;
+                        ++ct;
+                        cs = ct < T ? omp_start(ct, n, T) : 0x7fffffff;
+                    }
+                    if (it + 1 == cs) {  // the next chunk's first pixel sees this pre-pass vector
 #pragma unroll
-                    for (int j = 0; j < J; ++j) qorig[j] = s.p[j];
-                    mqorig = vec_min_bits<J>(s.p);
-                }
-                const bool masked = MASK && s.mk == 0;  // :824, :862
-                if (!(masked || mq == 0u)) {            // :880-881 -- else p stays untouched
-                    partial_opt<J>(s.p, q, mq, s.d1, s, sh, rev, lane, C);
-                    if (store) {
-#pragma unroll
-                        for (int j = 0; j < J; ++j) {
-                            const int qq = lane + 64 * j;
-                            if (qq < C.Q) *reinterpret_cast<f32x4*>(base + (size_t)pos * es + 4 * qq) = s.p[j];
-                        }
+                        for (int j = 0; j < J; ++j) qorig[j] = s.p[j];
+                        mqorig = vec_min_bits<J>(s.p);
                     }
                 }
+                const bool masked = MASK && __builtin_amdgcn_readfirstlane(s.mk) == 0;  // :824, :862
+                // :880-881: m == 0 leaves p untouched (branch-free: compute, then select)
+                f32x4 np[J];
 #pragma unroll
-                for (int j = 0; j < J; ++j) q[j] = s.p[j];
+                for (int j = 0; j < J; ++j) np[j] = s.p[j];
+                const int d1 = __builtin_amdgcn_readfirstlane(s.d1);
+                partial_opt<J>(np, q, mq, d1, s, psel0 + sh * 0x01010101u, lane, C);
+                const bool upd = !(masked || mq == 0u);
+#pragma unroll
+                for (int j = 0; j < J; ++j) q[j] = upd ? np[j] : s.p[j];
+                if (store && upd) {  // untouched vectors are not rewritten
+#pragma unroll
+                    for (int j = 0; j < J; ++j)
+#ifdef TSM_EXP_SCAN_NOSTORE
+                        if (q[j].x == -7.f)  // timing experiment only
+#endif
+                        *reinterpret_cast<f32x4*>(cur[j]) = q[j];
+                }
+#pragma unroll
+                for (int j = 0; j < J; ++j) cur[j] += dstep[j];
                 mq = vec_min_bits<J>(q);
                 if (WTA) {
                     const int d = vec_argmin<J>(q, lane, C.L, C.minD, mq);
                     if (lane == 0) wrow[pos] = d;
+                }
+                // refill this slot only now that its data is consumed (a load into a live
+                // slot would make the compiler stage it in temporaries and copy it back,
+                // waiting for the load right away)
+                scan_issue<J, HORIZ, MASK>(ring[k], posbase + dir * pfi, dir, line, pf, gv, R, orow, sgn, C);
+                if (pfi + 1 < n) {
+                    ++pfi;
+#pragma unroll
+                    for (int j = 0; j < J; ++j) pf[j] += dstep[j];
                 }
             }
         }
@@ -336,8 +394,12 @@ template <int J, bool HORIZ, bool MASK, bool WTA>
 static void launch_scan_t(float* vol, const uint8_t* grad, const uint32_t* img, int dir, int32_t* wta,
                           int store_view1, const float* infvec, const DevParams& P, hipStream_t st) {
     dim3 g(((HORIZ ? P.H : P.W) + 3) / 4, 2);
-    hipLaunchKernelGGL((k_scan_line<J, HORIZ, MASK, WTA>), g, dim3(256), 0, st, vol, grad, img, dir, wta,
-                       store_view1, infvec, P);
+    if (P.omp_threads > 1)
+        hipLaunchKernelGGL((k_scan_line<J, HORIZ, MASK, WTA, true>), g, dim3(256), 0, st, vol, grad, img, dir,
+                           wta, store_view1, infvec, P);
+    else
+        hipLaunchKernelGGL((k_scan_line<J, HORIZ, MASK, WTA, false>), g, dim3(256), 0, st, vol, grad, img, dir,
+                           wta, store_view1, infvec, P);
 }
 
 template <bool HORIZ, bool WTA>

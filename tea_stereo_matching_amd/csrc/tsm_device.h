@@ -86,19 +86,26 @@ constexpr int DPP_WAVE_SHR1 = 0x138;    // lane l <- lane l-1
 // Wave-wide min of NON-NEGATIVE floats (cost values), result uniform in every lane.
 // Non-negative IEEE floats order like their bit patterns, so the whole reduction runs
 // as unsigned integer min (DPP within rows, scalar across the four rows): exact, and
-// without the canonicalising v_max the compiler puts in front of every fminf.
-__device__ __forceinline__ float wave_min_nonneg(float x) {
-    uint32_t v = __float_as_uint(x);
-    const uint32_t inf = 0x7f800000u;
-    v = min(v, dpp_u<DPP_QUAD_1032>(v, inf));
-    v = min(v, dpp_u<DPP_QUAD_2301>(v, inf));
-    v = min(v, dpp_u<DPP_ROW_HALF_MIRROR>(v, inf));
-    v = min(v, dpp_u<DPP_ROW_MIRROR>(v, inf));
+// without the canonicalising v_max the compiler puts in front of every fminf.  The row
+// steps read every lane (quad_perm / mirrors), so bound_ctrl DPP moves fold into
+// v_min_u32_dpp (one instruction per level).
+__device__ __forceinline__ uint32_t dpp_row_min(uint32_t v) {
+    v = min(v, (uint32_t)__builtin_amdgcn_mov_dpp((int)v, DPP_QUAD_1032, 0xF, 0xF, true));
+    v = min(v, (uint32_t)__builtin_amdgcn_mov_dpp((int)v, DPP_QUAD_2301, 0xF, 0xF, true));
+    v = min(v, (uint32_t)__builtin_amdgcn_mov_dpp((int)v, DPP_ROW_HALF_MIRROR, 0xF, 0xF, true));
+    v = min(v, (uint32_t)__builtin_amdgcn_mov_dpp((int)v, DPP_ROW_MIRROR, 0xF, 0xF, true));
+    return v;
+}
+__device__ __forceinline__ uint32_t wave_min_bits(uint32_t v) {
+    v = dpp_row_min(v);
     const uint32_t r0 = __builtin_amdgcn_readlane(v, 0);
     const uint32_t r1 = __builtin_amdgcn_readlane(v, 16);
     const uint32_t r2 = __builtin_amdgcn_readlane(v, 32);
     const uint32_t r3 = __builtin_amdgcn_readlane(v, 48);
-    return __uint_as_float(min(min(r0, r1), min(r2, r3)));
+    return min(min(r0, r1), min(r2, r3));
+}
+__device__ __forceinline__ float wave_min_nonneg(float x) {
+    return __uint_as_float(wave_min_bits(__float_as_uint(x)));
 }
 
 // Wave-wide min of u64 keys (e.g. (float_bits << 32) | d for WTA first-min).
