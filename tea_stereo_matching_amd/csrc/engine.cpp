@@ -495,12 +495,13 @@ int run_pipeline(tsm_adc* h, Workspace* w, const uint8_t* d_left, const uint8_t*
     }
     mark();
     if (dump && dump->cost_agg && (rc = dump_vol(dump->cost_agg, 2)) != TSM_OK) return rc;
-    // --- scanline (+ fused WTA in the last pass) -------------------------------------
+    // --- scanline, then WTA of both final volumes --------------------------------------
     const bool keep_view1 = dump && dump->cost_scan;
     if (launch_scan_vertical(w->vol, w->gv, w->img, +1, w->infvec, P, st) != 0 ||
         launch_scan_vertical(w->vol, w->gv, w->img, -1, w->infvec, P, st) != 0 ||
         launch_scan_horizontal(w->vol, w->gh, w->img, +1, nullptr, 1, w->infvec, P, st) != 0 ||
-        launch_scan_horizontal(w->vol, w->gh, w->img, -1, w->rb.disp0, keep_view1 ? 1 : 0, w->infvec, P, st) != 0)
+        launch_scan_horizontal(w->vol, w->gh, w->img, -1, nullptr, 1, w->infvec, P, st) != 0 ||
+        launch_wta(w->vol, w->rb.disp0, w->infvec, P, st) != 0)
         return fail(h, TSM_ERR_UNSUPPORTED, "scanline: label count");
     mark();
     if (keep_view1 && (rc = dump_vol(dump->cost_scan, 2)) != TSM_OK) return rc;

@@ -432,4 +432,53 @@ int launch_scan_horizontal(float* vol, const uint8_t* gh, const uint32_t* img, i
     return launch_scan<true, false>(vol, gh, img, dir, nullptr, store_view1, infvec, P, st);
 }
 
+// ---------------------------------------------------------------------------
+// WTA (cost2disparity, ADCensus.cpp:1394-1413) over the final volumes of both views,
+// as its own memory-bound launch: one wave takes WTA_PX consecutive pixel vectors
+// (views are contiguous: pixel g of [2][H][W] is vector g), all loads in flight first.
+// Keeping the argmin out of the serial leftward pass shortens that pass's chain more
+// than re-reading the volumes costs.
+// ---------------------------------------------------------------------------
+constexpr int WTA_PX = 8;
+
+template <int J>
+__global__ __launch_bounds__(256) void k_wta(const float* __restrict__ vol, int32_t* __restrict__ disp,
+                                             const float* __restrict__ infvec, DevParams Pk) {
+    const DevParams P = Pk;
+    const int lane = threadIdx.x & 63;
+    const size_t npx = (size_t)2 * P.H * P.W;
+    const size_t g0 = ((size_t)blockIdx.x * 4 + (threadIdx.x >> 6)) * WTA_PX;
+    if (g0 >= npx) return;
+    const int Q = P.Lp >> 2;
+    f32x4 x[WTA_PX][J];
+#pragma unroll
+    for (int i = 0; i < WTA_PX; ++i) {
+        const size_t g = g0 + i < npx ? g0 + i : npx - 1;
+#pragma unroll
+        for (int j = 0; j < J; ++j) {
+            const int q = lane + 64 * j;
+            x[i][j] = *reinterpret_cast<const f32x4*>(q < Q ? vol + g * P.Lp + 4 * q : infvec);
+        }
+    }
+    int res = 0;
+#pragma unroll
+    for (int i = 0; i < WTA_PX; ++i) {
+        const uint32_t m = vec_min_bits<J>(x[i]);
+        const int d = vec_argmin<J>(x[i], lane, P.L, P.minD, m);
+        res = lane == i ? d : res;
+    }
+    if (lane < WTA_PX && g0 + lane < npx) disp[g0 + lane] = res;
+}
+
+int launch_wta(const float* vol, int32_t* disp, const float* infvec, const DevParams& P, hipStream_t st) {
+    const int J = (P.Lp / 4 + 63) / 64;
+    const size_t npx = (size_t)2 * P.H * P.W;
+    const dim3 g((unsigned)((npx + 4 * WTA_PX - 1) / (4 * WTA_PX)));
+    if (J == 1) hipLaunchKernelGGL((k_wta<1>), g, dim3(256), 0, st, vol, disp, infvec, P);
+    else if (J == 2) hipLaunchKernelGGL((k_wta<2>), g, dim3(256), 0, st, vol, disp, infvec, P);
+    else return -1;
+    trace_point("k_wta", st);
+    return 0;
+}
+
 }  // namespace tsm

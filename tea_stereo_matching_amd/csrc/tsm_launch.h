@@ -48,6 +48,8 @@ int launch_scan_vertical(float* vol, const uint8_t* gv, const uint32_t* img, int
 int launch_scan_horizontal(float* vol, const uint8_t* gh, const uint32_t* img, int dir,
                            int32_t* wta, int store_view1, const float* infvec, const DevParams& P,
                            hipStream_t st);
+// WTA of both views' final volumes into wta[2][H][W]
+int launch_wta(const float* vol, int32_t* wta, const float* infvec, const DevParams& P, hipStream_t st);
 
 // k_refine.hip
 struct RefineBufs {
