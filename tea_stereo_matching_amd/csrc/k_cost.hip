@@ -217,7 +217,7 @@ __device__ unsigned long long g_stamps[65536 * 8];
 #define CW_STAMP(i) do { } while (0)
 #endif
 
-template <int E, bool HSI, bool MASK>
+template <int E, bool HSI, bool MASK, bool SHEAR>
 __global__ __launch_bounds__(CW_THREADS) void k_cost_walk(
     const uint32_t* __restrict__ desc, const float* __restrict__ lutA, int lutA_n,
     const float* __restrict__ lutB, float* __restrict__ vol, DevParams Pk, int seg_len, int nseg,
@@ -238,7 +238,7 @@ __global__ __launch_bounds__(CW_THREADS) void k_cost_walk(
     // one walk unit (view, row, segment) per wave; the unit's loads (ring prologue and
     // warm-up gather) are issued before the table fill's barrier so their latencies overlap
     const int gw0 = blockIdx.x * (CW_THREADS / 64) + wave;
-    const bool active = gw0 < 2 * H * nseg;
+    const bool active = gw0 < (SHEAR ? 1 : 2) * H * nseg;  // SHEAR: view-0 units only
     const int gw = active ? gw0 : 0;
     CW_STAMP(0);
 #ifdef TSM_EXP_STAMPS
@@ -254,8 +254,17 @@ __global__ __launch_bounds__(CW_THREADS) void k_cost_walk(
     const int v = row / H, y = row - v * H;
     const int foff = v == 0 ? -P.minD : P.minD;
     const int x_lo = seg * seg_len;
-    const int count = min(seg_len, W - x_lo);
-    const int j0 = x_lo;  // both views walk j upward: stores stream forward through HBM
+    const int count0 = min(seg_len, W - x_lo);
+    // SHEAR (minD = 0): view 1 is an exact shear of view 0, C1(x1, k) = C0(x1 + k, k), so
+    // the view-0 walk also emits view 1.  Lane l completes the float4 of view-1 pixel
+    // x1 = j - 4l - 3 (labels 4l..4l+3 come from steps j-3..j); a unit therefore starts
+    // one group early (pre: those steps only fill the delay line) and the row's last unit
+    // runs one group past the image (post: border cells, 2 / +inf, finish the float4s
+    // that straddle the right edge).
+    const int pre = (SHEAR && seg > 0) ? E : 0;
+    const int post = (SHEAR && seg == nseg - 1) ? E : 0;
+    const int count = pre + count0 + post;  // steps walked
+    const int j0 = x_lo - pre;  // both views walk j upward: stores stream forward through HBM
     const int vtop = E * 64 - 1;  // view 1 feeds its shift register at the top label
     const int hw = P.censusW >> 1, hh = P.censusH >> 1;
     const bool rowOut = y - hh < 0 || y + hh >= H;
@@ -274,7 +283,7 @@ __global__ __launch_bounds__(CW_THREADS) void k_cost_walk(
     // (global_load_lds_dwordx4: lane i's 16 bytes land at chunk base + 16 i, i.e. record
     // i/4, quarter i%4; no staging registers): per step they are broadcast LDS reads,
     // never an L2/HBM round trip.
-    const int slots = cost_stage_slots(seg_len, E);
+    const int slots = cost_stage_slots(seg_len + (SHEAR ? 2 * E : 0), E);
     u32x4* stF = smem_stage + (size_t)wave * 2 * slots * 4;
     u32x4* stE = stF + (size_t)slots * 4;
     const int rq = lane & 3, rr = lane >> 2;  // this lane's quarter / record of a chunk
@@ -338,6 +347,10 @@ __global__ __launch_bounds__(CW_THREADS) void k_cost_walk(
     for (int e = 0; e < E; ++e) padoff[e] = (!MASK && E * lane + e >= L) ? CW_LUTB : 0u;
     // fixed records double-buffered by step parity (compile-time), no register copies
     uint32_t FA[NW], FB[NW], En[NW];
+    float dl0[4], dl1[4], dl2[4];  // SHEAR delay line (slots by step rotation)
+#pragma unroll
+    for (int i = 0; i < 4; ++i) dl0[i] = dl1[i] = dl2[i] = 0.f;
+    float* o1row = vol + ((size_t)H + y) * W * Lp;  // view-1 row (SHEAR)
     load_staged(stF, 0, FA);
 
     // one step at rotation R
@@ -414,16 +427,32 @@ __global__ __launch_bounds__(CW_THREADS) void k_cost_walk(
 #pragma unroll
             for (int e = 1; e < E; ++e) c[e] = E * lane + e >= L ? kInf : c[e];
         }
+        const bool own = SHEAR ? (t >= pre && t < pre + count0) : (fast || t < count);
 #ifdef TSM_EXP_NOSTORE
-        if ((fast || t < count) && c[0] == -12345.f) {
+        if (own && c[0] == -12345.f) {
 #else
-        if (fast || t < count) {
+        if (own) {
 #endif
 #pragma unroll
             for (int q = 0; q < E / 4; ++q)
                 if (E * lane + 4 * q < Lp)
                     *reinterpret_cast<f32x4*>(orow + (size_t)j * Lp + 4 * q) =
                         f32x4{c[4 * q], c[4 * q + 1], c[4 * q + 2], c[4 * q + 3]};
+        }
+        if constexpr (SHEAR) {
+            // delay line by step rotation (compile-time slots): element e of the float4
+            // completed now was computed 3 - e steps ago
+            dl0[R & 3] = c[0];
+            dl1[R & 3] = c[1];
+            dl2[R & 3] = c[2];
+            const int x1 = j - 4 * lane - 3;
+#ifdef TSM_EXP_NOSTORE1
+            if (t >= pre && x1 >= 0 && x1 < W && 4 * lane < Lp && c[3] == -12345.f)  // timing only
+#else
+            if (t >= pre && x1 >= 0 && x1 < W && 4 * lane < Lp)
+#endif
+                *reinterpret_cast<f32x4*>(o1row + (size_t)x1 * Lp + 4 * lane) =
+                    f32x4{dl0[(R + 1) & 3], dl1[(R + 2) & 3], dl2[(R + 3) & 3], c[3]};
         }
         // advance: view 0: the slot of offset E-1 becomes offset 0 of the next rotation,
         // fed from lane-1 (lane 0 has no source and keeps `old`, the entering word);
@@ -458,7 +487,7 @@ __global__ __launch_bounds__(CW_THREADS) void k_cost_walk(
         }
     }
     };
-    if (v == 0) walk(IC<0>{});
+    if (SHEAR || v == 0) walk(IC<0>{});
     else walk(IC<1>{});
     CW_STAMP(3);
 }
@@ -513,22 +542,48 @@ size_t cost_volume_lds_bytes(const DevParams& P, int lutA_n) {
     (void)P;
     (void)lutA_n;  // the tables are static LDS; this is the dynamic ring part
     const int E = P.Lp <= 256 ? 4 : 8;
-    return (size_t)(CW_THREADS / 64) * 2 * cost_stage_slots(cost_seg_len(P), E) * 64;
+    return (size_t)(CW_THREADS / 64) * 2 * cost_stage_slots(cost_seg_len(P) + 2 * E, E) * 64;
 }
 
-template <int E, bool HSI, bool MASK>
+// View-1 float4s the shear walk never completes: lane l of pixel x1 with x1 + 4l > W
+// (every label's left column x1 + k >= W: border cells, 2, or +inf padding).
+__global__ void k_shear_tail(float* __restrict__ vol, DevParams Pk) {
+    const DevParams P = Pk;
+    const int Q = P.Lp >> 2;
+    const int span = min(P.W, 4 * Q);  // x1 in [W - span, W)
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    const int y = blockIdx.y;
+    if (i >= span * Q) return;
+    const int x1 = P.W - span + i / Q, l = i % Q;
+    if (x1 + 4 * l <= P.W) return;
+    const float inf = __int_as_float(0x7f800000);
+    f32x4 o;
+    o.x = 4 * l + 0 < P.L ? 2.f : inf;
+    o.y = 4 * l + 1 < P.L ? 2.f : inf;
+    o.z = 4 * l + 2 < P.L ? 2.f : inf;
+    o.w = 4 * l + 3 < P.L ? 2.f : inf;
+    *reinterpret_cast<f32x4*>(vol + (((size_t)P.H + y) * P.W + x1) * P.Lp + 4 * l) = o;
+}
+
+template <int E, bool HSI, bool MASK, bool SHEAR>
 static void launch_cost_t(const uint32_t* desc, const float* lutA, int lutA_n, const float* lutB,
                           float* vol, const DevParams& P, uint32_t* ctr, uint32_t& ctr_base,
                           hipStream_t st) {
     const int seg_len = cost_seg_len(P);
     const int nseg = (P.W + seg_len - 1) / seg_len;
-    const int units = 2 * P.H * nseg;
+    const int units = (SHEAR ? 1 : 2) * P.H * nseg;
     const int waves = units;
     const int wpb = CW_THREADS / 64;
     dim3 g((waves + wpb - 1) / wpb);
-    hipLaunchKernelGGL((k_cost_walk<E, HSI, MASK>), g, dim3(CW_THREADS), cost_volume_lds_bytes(P, lutA_n), st,
-                       desc, lutA, lutA_n, lutB, vol, P, seg_len, nseg, ctr, ctr_base);
+    hipLaunchKernelGGL((k_cost_walk<E, HSI, MASK, SHEAR>), g, dim3(CW_THREADS), cost_volume_lds_bytes(P, lutA_n),
+                       st, desc, lutA, lutA_n, lutB, vol, P, seg_len, nseg, ctr, ctr_base);
     trace_point("k_cost_walk", st);
+    if (SHEAR) {
+        const int Q = P.Lp >> 2;
+        const int n = (P.W < 4 * Q ? P.W : 4 * Q) * Q;
+        hipLaunchKernelGGL(k_shear_tail, dim3((n + 255) / 256, P.H), dim3(256), 0, st, vol, P);
+        trace_point("k_shear_tail", st);
+    }
     ctr_base += (uint32_t)units + (uint32_t)(g.x * wpb);  // every wave overshoots once
 }
 
@@ -539,11 +594,25 @@ int launch_cost_volume(const uint32_t* img, const uint32_t* desc, const float* l
     const bool hsi = P.color_model == 1;
 #define CASE(E)                                                                                    \
     if (hsi) {                                                                                     \
-        if (P.mask) launch_cost_t<E, true, true>(desc, lutA, lutA_n, lutB, vol, P, ctr, ctr_base, st);  \
-        else launch_cost_t<E, true, false>(desc, lutA, lutA_n, lutB, vol, P, ctr, ctr_base, st);        \
+        if (P.mask) launch_cost_t<E, true, true, false>(desc, lutA, lutA_n, lutB, vol, P, ctr, ctr_base, st);  \
+        else launch_cost_t<E, true, false, false>(desc, lutA, lutA_n, lutB, vol, P, ctr, ctr_base, st);        \
     } else {                                                                                       \
-        if (P.mask) launch_cost_t<E, false, true>(desc, lutA, lutA_n, lutB, vol, P, ctr, ctr_base, st); \
-        else launch_cost_t<E, false, false>(desc, lutA, lutA_n, lutB, vol, P, ctr, ctr_base, st);       \
+        if (P.mask) launch_cost_t<E, false, true, false>(desc, lutA, lutA_n, lutB, vol, P, ctr, ctr_base, st); \
+        else launch_cost_t<E, false, false, false>(desc, lutA, lutA_n, lutB, vol, P, ctr, ctr_base, st);       \
+    }
+    // minD = 0 without mask mode: view 1 is an exact shear of view 0 and one walk can emit
+    // both (parity-green).  Off by default: its view-1 stores are 16-B scatters (one per
+    // lane, 64 different pixel vectors per instruction) and cost more than the second walk
+    // saves (MI355X, config B: 390 us vs 254 us; 149 us with the view-1 stores removed).
+    // TSM_COST_SHEAR=1 selects it.
+    static const bool shear = [] {
+        const char* e = getenv("TSM_COST_SHEAR");
+        return e && e[0] == '1';
+    }();
+    if (P.minD == 0 && !P.mask && P.Lp <= 256 && shear) {
+        if (hsi) launch_cost_t<4, true, false, true>(desc, lutA, lutA_n, lutB, vol, P, ctr, ctr_base, st);
+        else launch_cost_t<4, false, false, true>(desc, lutA, lutA_n, lutB, vol, P, ctr, ctr_base, st);
+        return 0;
     }
     // one wave holds the whole label axis: E labels per lane
     if (P.Lp <= 256) { CASE(4) }
