@@ -217,7 +217,12 @@ __device__ unsigned long long g_stamps[65536 * 8];
 #define CW_STAMP(i) do { } while (0)
 #endif
 
-template <int E, bool HSI, bool MASK, bool SHEAR>
+// MODE: CW_BOTH walks both views (unit -> view from the row index), CW_VIEW0 / CW_VIEW1
+// one view per launch (one walk direction per kernel: fewer VGPRs, more waves per SIMD),
+// CW_SHEAR the view-0 walk that also emits view 1.
+enum { CW_BOTH = 0, CW_VIEW0 = 1, CW_VIEW1 = 2, CW_SHEAR = 3 };
+
+template <int E, bool HSI, bool MASK, int MODE>
 __global__ __launch_bounds__(CW_THREADS) void k_cost_walk(
     const uint32_t* __restrict__ desc, const float* __restrict__ lutA, int lutA_n,
     const float* __restrict__ lutB, float* __restrict__ vol, DevParams Pk, int seg_len, int nseg,
@@ -238,7 +243,8 @@ __global__ __launch_bounds__(CW_THREADS) void k_cost_walk(
     // one walk unit (view, row, segment) per wave; the unit's loads (ring prologue and
     // warm-up gather) are issued before the table fill's barrier so their latencies overlap
     const int gw0 = blockIdx.x * (CW_THREADS / 64) + wave;
-    const bool active = gw0 < (SHEAR ? 1 : 2) * H * nseg;  // SHEAR: view-0 units only
+    constexpr bool SHEAR = MODE == CW_SHEAR;
+    const bool active = gw0 < (MODE == CW_BOTH ? 2 : 1) * H * nseg;
     const int gw = active ? gw0 : 0;
     CW_STAMP(0);
 #ifdef TSM_EXP_STAMPS
@@ -251,7 +257,8 @@ __global__ __launch_bounds__(CW_THREADS) void k_cost_walk(
 #endif
     const int seg = gw % nseg;
     const int row = gw / nseg;
-    const int v = row / H, y = row - v * H;
+    const int v = MODE == CW_BOTH ? row / H : (MODE == CW_VIEW1 ? 1 : 0);
+    const int y = MODE == CW_BOTH ? row - v * H : row;
     const int foff = v == 0 ? -P.minD : P.minD;
     const int x_lo = seg * seg_len;
     const int count0 = min(seg_len, W - x_lo);
@@ -487,8 +494,14 @@ __global__ __launch_bounds__(CW_THREADS) void k_cost_walk(
         }
     }
     };
-    if (SHEAR || v == 0) walk(IC<0>{});
-    else walk(IC<1>{});
+    if constexpr (MODE == CW_VIEW0 || MODE == CW_SHEAR) {
+        walk(IC<0>{});
+    } else if constexpr (MODE == CW_VIEW1) {
+        walk(IC<1>{});
+    } else {
+        if (v == 0) walk(IC<0>{});
+        else walk(IC<1>{});
+    }
     CW_STAMP(3);
 }
 
@@ -565,26 +578,45 @@ __global__ void k_shear_tail(float* __restrict__ vol, DevParams Pk) {
     *reinterpret_cast<f32x4*>(vol + (((size_t)P.H + y) * P.W + x1) * P.Lp + 4 * l) = o;
 }
 
-template <int E, bool HSI, bool MASK, bool SHEAR>
+template <int E, bool HSI, bool MASK, int MODE>
 static void launch_cost_t(const uint32_t* desc, const float* lutA, int lutA_n, const float* lutB,
                           float* vol, const DevParams& P, uint32_t* ctr, uint32_t& ctr_base,
                           hipStream_t st) {
     const int seg_len = cost_seg_len(P);
     const int nseg = (P.W + seg_len - 1) / seg_len;
-    const int units = (SHEAR ? 1 : 2) * P.H * nseg;
+    const int units = (MODE == CW_BOTH ? 2 : 1) * P.H * nseg;
     const int waves = units;
     const int wpb = CW_THREADS / 64;
     dim3 g((waves + wpb - 1) / wpb);
-    hipLaunchKernelGGL((k_cost_walk<E, HSI, MASK, SHEAR>), g, dim3(CW_THREADS), cost_volume_lds_bytes(P, lutA_n),
+    hipLaunchKernelGGL((k_cost_walk<E, HSI, MASK, MODE>), g, dim3(CW_THREADS), cost_volume_lds_bytes(P, lutA_n),
                        st, desc, lutA, lutA_n, lutB, vol, P, seg_len, nseg, ctr, ctr_base);
     trace_point("k_cost_walk", st);
-    if (SHEAR) {
+    if (MODE == CW_SHEAR) {
         const int Q = P.Lp >> 2;
         const int n = (P.W < 4 * Q ? P.W : 4 * Q) * Q;
         hipLaunchKernelGGL(k_shear_tail, dim3((n + 255) / 256, P.H), dim3(256), 0, st, vol, P);
         trace_point("k_shear_tail", st);
     }
     ctr_base += (uint32_t)units + (uint32_t)(g.x * wpb);  // every wave overshoots once
+}
+
+// One launch walking both views (default), or -- TSM_COST_VIEWS=1 -- one launch per view,
+// each kernel holding one walk direction (101-109 instead of 157 VGPRs, but the second
+// launch's ramp costs more than the occupancy gains: 265 vs 255 us on config B).
+template <int E, bool HSI, bool MASK>
+static void launch_cost_views(const uint32_t* desc, const float* lutA, int lutA_n, const float* lutB,
+                              float* vol, const DevParams& P, uint32_t* ctr, uint32_t& ctr_base,
+                              hipStream_t st) {
+    static const bool both = [] {
+        const char* e = getenv("TSM_COST_VIEWS");
+        return !(e && e[0] == '1');
+    }();
+    if (both) {
+        launch_cost_t<E, HSI, MASK, CW_BOTH>(desc, lutA, lutA_n, lutB, vol, P, ctr, ctr_base, st);
+        return;
+    }
+    launch_cost_t<E, HSI, MASK, CW_VIEW0>(desc, lutA, lutA_n, lutB, vol, P, ctr, ctr_base, st);
+    launch_cost_t<E, HSI, MASK, CW_VIEW1>(desc, lutA, lutA_n, lutB, vol, P, ctr, ctr_base, st);
 }
 
 int launch_cost_volume(const uint32_t* img, const uint32_t* desc, const float* lutA, int lutA_n,
@@ -594,11 +626,11 @@ int launch_cost_volume(const uint32_t* img, const uint32_t* desc, const float* l
     const bool hsi = P.color_model == 1;
 #define CASE(E)                                                                                    \
     if (hsi) {                                                                                     \
-        if (P.mask) launch_cost_t<E, true, true, false>(desc, lutA, lutA_n, lutB, vol, P, ctr, ctr_base, st);  \
-        else launch_cost_t<E, true, false, false>(desc, lutA, lutA_n, lutB, vol, P, ctr, ctr_base, st);        \
+        if (P.mask) launch_cost_views<E, true, true>(desc, lutA, lutA_n, lutB, vol, P, ctr, ctr_base, st);  \
+        else launch_cost_views<E, true, false>(desc, lutA, lutA_n, lutB, vol, P, ctr, ctr_base, st);        \
     } else {                                                                                       \
-        if (P.mask) launch_cost_t<E, false, true, false>(desc, lutA, lutA_n, lutB, vol, P, ctr, ctr_base, st); \
-        else launch_cost_t<E, false, false, false>(desc, lutA, lutA_n, lutB, vol, P, ctr, ctr_base, st);       \
+        if (P.mask) launch_cost_views<E, false, true>(desc, lutA, lutA_n, lutB, vol, P, ctr, ctr_base, st); \
+        else launch_cost_views<E, false, false>(desc, lutA, lutA_n, lutB, vol, P, ctr, ctr_base, st);       \
     }
     // minD = 0 without mask mode: view 1 is an exact shear of view 0 and one walk can emit
     // both (parity-green).  Off by default: its view-1 stores are 16-B scatters (one per
@@ -610,8 +642,8 @@ int launch_cost_volume(const uint32_t* img, const uint32_t* desc, const float* l
         return e && e[0] == '1';
     }();
     if (P.minD == 0 && !P.mask && P.Lp <= 256 && shear) {
-        if (hsi) launch_cost_t<4, true, false, true>(desc, lutA, lutA_n, lutB, vol, P, ctr, ctr_base, st);
-        else launch_cost_t<4, false, false, true>(desc, lutA, lutA_n, lutB, vol, P, ctr, ctr_base, st);
+        if (hsi) launch_cost_t<4, true, false, CW_SHEAR>(desc, lutA, lutA_n, lutB, vol, P, ctr, ctr_base, st);
+        else launch_cost_t<4, false, false, CW_SHEAR>(desc, lutA, lutA_n, lutB, vol, P, ctr, ctr_base, st);
         return 0;
     }
     // one wave holds the whole label axis: E labels per lane
