@@ -178,7 +178,7 @@ size_t workspace_bytes(int H, int W, int L) {
     b += 2 * N * 16 * 4;       // desc
     b += 2 * N * Lp * 4;       // vol
     b += 2 * N * 4 + 256;      // arms, cost-walk counter
-    b += 4 * N * 4;            // ws
+    b += 12 * N * 4;           // ws, reciprocals, packed descriptors
     b += 4 * (size_t)H * (W + 2 * grad_pad(L) + 16);  // gv, gh (upper bound)
     b += N * (4 * 8 + 2 * 20 + 1 * 6 + 2 * 2 + 4); // refine maps
     return b;
@@ -284,7 +284,7 @@ int ensure_workspace(tsm_adc* h, Workspace* w, int H, int W) {
     A(w->arms, 2 * N * 4);
     A(w->cost_ctr, 256);
     A(w->infvec, 256);
-    A(w->ws, 4 * N * 4);
+    A(w->ws, 12 * N * 4);  // window sizes, reciprocals, packed descriptors (k_window_sizes)
     {
         const int gp = grad_pad(h->max_disparity);
         const size_t gs = (size_t)(((W + 2 * gp + 15) / 16) * 16);
@@ -483,7 +483,7 @@ int run_pipeline(tsm_adc* h, Workspace* w, const uint8_t* d_left, const uint8_t*
                               passes[i + 1].horizontal == a.horizontal;
             int rcp = -1;
             if (kind == 0) {
-                rcp = launch_agg_stream(w->vol, w->arms, a.ws, a.horizontal, pair, P, st);
+                rcp = launch_agg_stream(w->vol, w->arms, a.ws, w->ws, a.horizontal, pair, P, st);
                 if (rcp == 0 && pair) ++i;
             } else if (kind == 2) {
                 rcp = launch_agg_pass(w->vol, w->arms, a.ws, a.horizontal, pair, P, st);

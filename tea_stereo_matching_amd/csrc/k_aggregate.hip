@@ -105,6 +105,16 @@ __global__ void k_window_sizes(const uint32_t* __restrict__ arms, int32_t* __res
     }
     ws[((size_t)(v * 2 + 0) * H + y) * W + x] = hf;
     ws[((size_t)(v * 2 + 1) * H + y) * W + x] = vf;
+    // For the split streamer, per pass direction d (0 vertical: divides by hf, 1 horizontal:
+    // by vf), same [v][d][H][W] layout: ws + 4HW the correctly rounded reciprocals of the
+    // window sizes, ws + 8HW the packed descriptor lo | hi << 8 | size << 16.
+    float* rcp = reinterpret_cast<float*>(ws + (size_t)4 * H * W);
+    uint32_t* pk = reinterpret_cast<uint32_t*>(ws + (size_t)8 * H * W);
+    const size_t i0 = ((size_t)(v * 2 + 0) * H + y) * W + x, i1 = ((size_t)(v * 2 + 1) * H + y) * W + x;
+    rcp[i0] = 1.0f / (float)hf;
+    rcp[i1] = 1.0f / (float)vf;
+    pk[i0] = (a & 0xffffu) | ((uint32_t)hf << 16);
+    pk[i1] = (a >> 16) | ((uint32_t)vf << 16);
 }
 
 // colour differences between vertical / horizontal neighbours of each view image,
@@ -691,9 +701,8 @@ __device__ __forceinline__ f32x4 div_ws(f32x4 a, float b, float y) {
     const f32x4 r = __builtin_elementwise_fma(-q0, f32x4{b, b, b, b}, a);
     f32x4 q = __builtin_elementwise_fma(r, f32x4{y, y, y, y}, q0);
     // 0 < a < 2^-40 (never seen in practice) takes the IEEE path; a == 0 is exact above
-    const u32x4 ab = __builtin_bit_cast(u32x4, a) - 1u;
-    const uint32_t lim = 0x2b800000u - 1u;
-    if (__builtin_expect(ab.x < lim || ab.y < lim || ab.z < lim || ab.w < lim, 0)) {
+    const u32x4 ab = __builtin_bit_cast(u32x4, a) - 1u;  // +0 wraps to 0xffffffff
+    if (__builtin_expect(min(min(ab.x, ab.y), min(ab.z, ab.w)) < 0x2b800000u - 1u, 0)) {
         q.x = a.x / b; q.y = a.y / b; q.z = a.z / b; q.w = a.w / b;
     }
     return q;
@@ -709,6 +718,8 @@ struct AggStream {
     float* vol;
     const uint32_t* arms;
     const int32_t* ws;     // window sizes of the dividing pass (nullptr: no divide)
+    const uint32_t* pk;    // split streamer: packed descriptors of this direction, view 0
+    const float* rcp;      // split streamer: reciprocals of this direction, view 0
     int horizontal;
     int n;                 // pixels per line
     int cpl;               // chunks per line
@@ -1019,6 +1030,270 @@ __global__ __launch_bounds__(AS_THREADS) void k_agg_stream(AggStream S, DevParam
     AST_FLUSH();
 }
 
+// ---------------------------------------------------------------------------
+// 1-D aggregation v6: role-split persistent streamer (the default)
+// ---------------------------------------------------------------------------
+// Same stream, rings and window descriptors as v5, but the 16 waves of a workgroup split
+// by role so a step's two window sums run in parallel and no wave ever mixes loads with
+// stores (the compiler drains vmcnt(0) whenever a wave with stores in flight consumes a
+// load):
+//   A waves (8): wave w owns pixel w of every chunk.  It stages its own pixel vectors
+//     AX_D steps ahead in a VGPR ring (one 16-B-per-lane load and two meta words per step,
+//     counted vmcnt waits, no stores), copies pixel w of chunk s + AHEAD into ring1,
+//     writes its window descriptor, and sums pass A of chunk s into ring2.
+//   B waves (8): pass B of chunk s - LAG over ring2 (FUSED), or the copy of pass A's
+//     chunk s - 1 out of ring2 (single pass), and the stores to HBM.
+// One barrier per step; every wave runs the same whole number of AX_D-step blocks.
+constexpr int AX_THREADS = 16 * 64;
+constexpr int AX_MW = 2;  // meta words per pixel: packed descriptor (lo, hi, size), RN(1/size)
+constexpr int AX_D = 12;  // A-wave staging ring: steps in flight (AX_D * 8 px * Q * 16 B per CU)
+
+template <bool FUSED, int QT>
+__global__ __launch_bounds__(AX_THREADS) void k_agg_split(AggStream S, DevParams Pk) {
+    const DevParams P = Pk;
+    extern __shared__ __attribute__((aligned(16))) f32x4 smem_f4[];
+    const int H = P.H, W = P.W, Lp = P.Lp;
+    const int Q = QT > 0 ? QT : Lp >> 2;
+    const uint32_t Qs = (uint32_t)Q * 16;                                // bytes per ring pixel
+    const size_t vstride = (size_t)H * W * Lp;
+    const size_t es = S.horizontal ? (size_t)Lp : (size_t)W * Lp;         // floats per pixel step
+    const size_t ls = S.horizontal ? (size_t)W * Lp : (size_t)Lp;          // floats per line step
+    const size_t aes = S.horizontal ? 1 : (size_t)W;
+    const size_t als = S.horizontal ? (size_t)W : 1;
+    const int shA = S.horizontal ? 16 : 0, shB = S.horizontal ? 24 : 8;
+    const int g = blockIdx.x, G = gridDim.x;
+    const int my_lines = (S.nl - g + G - 1) / G;
+    const int nch = my_lines * S.cpl;
+    const uint32_t r1_off = 0;                                            // LDS byte offsets
+    const uint32_t r2_off = (uint32_t)AS_RP1 * Qs;
+    const uint32_t meta_off = r2_off + (uint32_t)AS_RP2 * Qs;
+    const uint32_t zero_off = meta_off + (uint32_t)AS_MC * AS_SEG * AX_MW * 4;
+    const uint32_t r1_end = r1_off + (uint32_t)AS_RP1 * Qs, r2_end = r2_off + (uint32_t)AS_RP2 * Qs;
+    char* lds = reinterpret_cast<char*>(smem_f4);
+
+    const int tid = threadIdx.x;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int lane = tid & 63;
+    const bool roleA = wave < AS_SEG;
+    const int w = roleA ? wave : wave - AS_SEG;  // pixel of the chunk this wave owns
+    const int nsteps = nch + (FUSED ? AS_LAG : 1);
+    const int nblk = (nsteps + AX_D - 1) / AX_D;  // every wave runs nblk * AX_D steps
+    const uint32_t lane16 = (uint32_t)lane * 16;
+    const bool vl = lane < Q;
+    auto line_base = [&](int lidx) -> size_t {
+        const int gl = g + lidx * G;
+        const int v = gl / S.nlv, line = gl - v * S.nlv;
+        return (size_t)v * vstride + (size_t)line * ls;
+    };
+    auto barrier = [&]() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); };
+    // sequential window sum of `len` ring pixels from LDS byte offset `off` in the ring
+    // [rb, re): blocks of 4 at immediate offsets while they do not wrap, then blocks whose
+    // slots past the window read the zero vector (x + 0.0 == x for the non-negative sums)
+    auto window = [&](uint32_t off, int len, uint32_t rb, uint32_t re) -> f32x4 {
+        f32x4 acc = f32x4{0.f, 0.f, 0.f, 0.f};
+        const char* lp = lds + lane16;
+        int j = 0;
+        for (; j + 4 <= len && off + 4 * Qs <= re; j += 4) {
+            const char* p = lp + off;
+            const f32x4 x0 = *reinterpret_cast<const f32x4*>(p);
+            const f32x4 x1 = *reinterpret_cast<const f32x4*>(p + Qs);
+            const f32x4 x2 = *reinterpret_cast<const f32x4*>(p + 2 * Qs);
+            const f32x4 x3 = *reinterpret_cast<const f32x4*>(p + 3 * Qs);
+            acc += x0;
+            acc += x1;
+            acc += x2;
+            acc += x3;
+            off += 4 * Qs;
+            off = off == re ? rb : off;
+        }
+        for (; j < len; j += 4) {
+            f32x4 x[4];
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                const uint32_t o = j + u < len ? off : zero_off;
+                x[u] = *reinterpret_cast<const f32x4*>(lp + o);
+                off += Qs;
+                off = off == re ? rb : off;
+            }
+#pragma unroll
+            for (int u = 0; u < 4; ++u) acc += x[u];
+        }
+        return acc;
+    };
+    const uint32_t mstep = AS_SEG * AX_MW * 4, mwrap = AS_MC * mstep;
+    const char* mbase = lds + meta_off + (uint32_t)w * AX_MW * 4;  // this wave's pixel column
+#ifdef TSM_EXP_STAMPS
+    unsigned long long ast[3] = {0, 0, 0};
+    const unsigned long long ast_t0 = __builtin_amdgcn_s_memtime();
+#endif
+
+    if (roleA) {
+        // ---- A: staging ring, land, pass A ----------------------------------------------
+        const int lanec = lane < Q ? lane : Q - 1;
+        const __amdgpu_buffer_rsrc_t rs_vol = make_rsrc(S.vol), rs_pk = make_rsrc(S.pk),
+                                     rs_rcp = make_rsrc(S.rcp);
+        const uint32_t voff = (uint32_t)lanec * 16;
+        const uint32_t es4 = (uint32_t)(es * 4), aes4 = (uint32_t)(aes * 4);
+        // the meta words are uniform; an opaque zero lane offset keeps them in VGPRs
+        // (uniform values would be moved to SGPRs right after the load: a wait per load)
+        uint32_t vzero;
+        asm volatile("v_mov_b32 %0, 0" : "=v"(vzero));
+        // issue position (chunk ci = s + AHEAD + AX_D at step s), advanced one chunk a step
+        int il = 0, icc = 0;
+        uint32_t iv = 0, ia = 0;  // byte offsets of line il: vol, descriptors (= reciprocals)
+        auto set_line = [&]() {
+            const int gl = g + il * G;
+            const int v = gl / S.nlv, line = gl - v * S.nlv;
+            iv = (uint32_t)(((size_t)v * vstride + (size_t)line * ls) * 4);
+            ia = (uint32_t)(2 * v * H * W + line * (int)als) * 4;  // per-view stride 2HW
+        };
+        set_line();
+        f32x4 rv[AX_D];
+        uint32_t rma[AX_D], rmy[AX_D];  // packed descriptor, RN(1/size) bits
+        auto issue = [&](int k) {  // chunk at (il, icc) -> slot k; past the end: re-read the last pixel
+            const bool past = il >= my_lines;
+            const uint32_t pos = past ? (uint32_t)(S.n - 1) : (uint32_t)min(icc * AS_SEG + w, S.n - 1);
+            rv[k] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rs_vol, voff, iv + pos * es4, 0));
+            rma[k] = (uint32_t)__builtin_amdgcn_raw_buffer_load_b32(rs_pk, vzero, ia + pos * aes4, 0);
+            rmy[k] = S.ws ? (uint32_t)__builtin_amdgcn_raw_buffer_load_b32(rs_rcp, vzero, ia + pos * aes4, 0) : vzero;
+            if (!past && ++icc == S.cpl) {
+                icc = 0;
+                ++il;
+                if (il < my_lines) set_line();
+            }
+        };
+        // pixel w of chunk c -> ring1; its raw descriptor (arms, window size, reciprocal)
+        // -> the meta ring (every lane writes the same 16 B: no exec branch)
+        auto land = [&](const f32x4& val, uint32_t ma, uint32_t my, int c) {
+            *reinterpret_cast<f32x4*>(lds + r1_off + (uint32_t)((c % AS_RC1) * AS_SEG + w) * Qs + voff) = val;
+            *reinterpret_cast<u32x2*>(lds + meta_off + (uint32_t)((c % AS_MC) * AS_SEG + w) * AX_MW * 4) = u32x2{ma, my};
+        };
+        // prologue: chunks 0 .. AHEAD + AX_D - 1 in flight, chunks 0 .. AHEAD - 1 landed.
+        // Slot of chunk c: (c - AHEAD) mod AX_D, so step s lands and refills slot s mod AX_D.
+        f32x4 pre[AS_AHEAD];
+        uint32_t pma[AS_AHEAD], pmy[AS_AHEAD];
+#pragma unroll
+        for (int c = 0; c < AS_AHEAD; ++c) {
+            issue(0);
+            pre[c] = rv[0];
+            pma[c] = rma[0];
+            pmy[c] = rmy[0];
+        }
+#pragma unroll
+        for (int k = 0; k < AX_D; ++k) issue(k);
+#pragma unroll
+        for (int c = 0; c < AS_AHEAD; ++c) land(pre[c], pma[c], pmy[c], c);
+        int ca = 0, cc_a = 0;  // pass-A chunk s: position in its line (validity of pixel w)
+        uint32_t r2w = r2_off + (uint32_t)w * Qs;  // ring2 slot of chunk s
+        uint32_t ma_off = 0;
+        int rp1 = w;  // ring1 pixel of chunk s, pixel w
+        u32x2 mA;
+        barrier();
+        mA = *reinterpret_cast<const u32x2*>(mbase + ma_off);
+        for (int b = 0; b < nblk; ++b) {
+#pragma unroll
+            for (int u = 0; u < AX_D; ++u) {
+                const int s = b * AX_D + u;
+                // land chunk s + AHEAD from slot u, then refill the slot (chunk s + AHEAD + AX_D)
+                AST_T(t0);
+                land(rv[u], rma[u], rmy[u], s + AS_AHEAD);
+                issue(u);
+                AST_T(t1);
+                AST_ADD(1, t1 - t0);
+                const uint32_t arm = __builtin_amdgcn_readfirstlane(mA.x);
+                const float a_y = __uint_as_float(__builtin_amdgcn_readfirstlane(mA.y));
+                const float a_b = (float)(int)(arm >> 16);
+                const int lo = (int)(arm & 0xffu), hi = (int)((arm >> 8) & 0xffu);
+                int st = rp1 - lo;
+                st = st < 0 ? st + AS_RP1 : st;
+                const uint32_t a_off = r1_off + (uint32_t)st * Qs;
+                const int a_len = lo + hi + 1;
+                rp1 = rp1 + AS_SEG >= AS_RP1 ? rp1 + AS_SEG - AS_RP1 : rp1 + AS_SEG;
+                ma_off += mstep;
+                ma_off = ma_off >= mwrap ? ma_off - mwrap : ma_off;
+                mA = *reinterpret_cast<const u32x2*>(mbase + ma_off);  // chunk s + 1 (landed)
+                if (s < nch && cc_a * AS_SEG + w < S.n) {
+                    f32x4 acc = window(a_off, a_len, r1_off, r1_end);
+                    if (S.ws) acc = div_ws(acc, a_b, a_y);
+                    if (vl) *reinterpret_cast<f32x4*>(lds + r2w + lane16) = acc;
+                }
+                if (++cc_a == S.cpl) cc_a = 0;
+                (void)ca;
+                r2w += AS_SEG * Qs;
+                r2w = r2w >= r2_end ? r2w - (uint32_t)AS_RP2 * Qs : r2w;
+                AST_T(t2);
+                AST_ADD(2, t2 - t1);
+                barrier();
+                AST_T(t3);
+                AST_ADD(0, t3 - t2);
+            }
+        }
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // no load outlives the workgroup
+        AST_FLUSH();
+        return;
+    }
+
+    // ---- B: pass B over ring2 (FUSED) or pass A's outputs out of ring2, stores ------------
+    struct Out {
+        int lidx, cc;
+        size_t off;
+    };
+    auto out_init = [&](Out& o) { o.lidx = 0; o.cc = 0; o.off = line_base(0) + (size_t)w * es; };
+    auto out_step = [&](Out& o) {
+        if (++o.cc == S.cpl) { o.cc = 0; ++o.lidx; if (o.lidx < my_lines) o.off = line_base(o.lidx) + (size_t)w * es; }
+        else o.off += (size_t)AS_SEG * es;
+    };
+    if (wave == AS_SEG && vl) *reinterpret_cast<f32x4*>(lds + zero_off + lane16) = f32x4{0.f, 0.f, 0.f, 0.f};
+    Out ob;
+    out_init(ob);
+    const int lag = FUSED ? AS_LAG : 1;
+    uint32_t mb_off = (uint32_t)((AS_MC - lag % AS_MC) % AS_MC) * mstep;  // meta of chunk s - lag
+    uint32_t r2r = r2_off + (uint32_t)(((AS_RC2 - 1) % AS_RC2) * AS_SEG + w) * Qs;  // single: chunk s - 1
+    barrier();
+    uint32_t mB = *reinterpret_cast<const uint32_t*>(mbase + mb_off);  // arms of chunk s - lag
+    int rp2 = (AS_RP2 - lag * AS_SEG % AS_RP2 + w) % AS_RP2;             // its ring2 pixel
+    for (int b = 0; b < nblk; ++b) {
+        for (int u = 0; u < AX_D; ++u) {
+            const int s = b * AX_D + u;
+            const uint32_t arm = __builtin_amdgcn_readfirstlane(mB);
+            const int lo = (int)(arm & 0xffu), hi = (int)((arm >> 8) & 0xffu);
+            int st = rp2 - lo;
+            st = st < 0 ? st + AS_RP2 : st;
+            const uint32_t b_off = r2_off + (uint32_t)st * Qs;
+            const int b_len = lo + hi + 1;
+            rp2 = rp2 + AS_SEG >= AS_RP2 ? rp2 + AS_SEG - AS_RP2 : rp2 + AS_SEG;
+            mb_off += mstep;
+            mb_off = mb_off >= mwrap ? mb_off - mwrap : mb_off;
+            mB = *reinterpret_cast<const uint32_t*>(mbase + mb_off);
+            const int sb = s - lag;
+            AST_T(t1);
+            if (sb >= 0 && sb < nch) {
+                if (ob.cc * AS_SEG + w < S.n) {
+                    const f32x4 acc = FUSED ? window(b_off, b_len, r2_off, r2_end)
+                                            : *reinterpret_cast<const f32x4*>(lds + r2r + lane16);
+                    if (vl) *reinterpret_cast<f32x4*>(S.vol + ob.off + 4 * lane) = acc;
+                }
+                out_step(ob);
+            }
+            if (!FUSED) {
+                r2r += AS_SEG * Qs;
+                r2r = r2r >= r2_end ? r2r - (uint32_t)AS_RP2 * Qs : r2r;
+            }
+            AST_T(t2);
+            AST_ADD(2, t2 - t1);
+            barrier();
+            AST_T(t3);
+            AST_ADD(0, t3 - t2);
+        }
+    }
+    AST_FLUSH();
+}
+
+static size_t agg_split_lds(const DevParams& P) {
+    const int Q = P.Lp / 4;
+    return ((size_t)AS_RP1 + AS_RP2 + 1) * Q * 16 + (size_t)AS_MC * AS_SEG * AX_MW * 4;
+}
+
 static size_t agg_stream_lds(const DevParams& P, bool fused) {
     const int Q = P.Lp / 4;
     return ((size_t)AS_RP1 + (fused ? AS_RP2 : 0) + 1) * Q * 16 + (size_t)AS_MC * AS_SEG * AS_MW * 4;
@@ -1031,8 +1306,8 @@ static void agg_stream_attrs() {
 }
 
 // Returns -1 if the streamer does not support the geometry (caller falls back).
-int launch_agg_stream(float* vol, const uint32_t* arms, const int32_t* ws, int horizontal, bool fused,
-                      const DevParams& P, hipStream_t st) {
+int launch_agg_stream(float* vol, const uint32_t* arms, const int32_t* ws, const int32_t* ws_base,
+                      int horizontal, bool fused, const DevParams& P, hipStream_t st) {
     const int Q = P.Lp / 4;
     if (Q > 64 || P.max_length1 - 1 > AS_MAX_ARM) return -1;
     if ((size_t)2 * P.H * P.W * P.Lp * 4 >= ((size_t)1 << 31)) return -1;  // 32-bit buffer offsets
@@ -1048,6 +1323,8 @@ int launch_agg_stream(float* vol, const uint32_t* arms, const int32_t* ws, int h
     S.vol = vol;
     S.arms = arms;
     S.ws = ws;
+    S.rcp = reinterpret_cast<const float*>(ws_base + (size_t)(4 + horizontal) * P.H * P.W);
+    S.pk = reinterpret_cast<const uint32_t*>(ws_base + (size_t)(8 + horizontal) * P.H * P.W);
     S.horizontal = horizontal;
     S.n = horizontal ? P.W : P.H;
     S.cpl = (S.n + AS_SEG - 1) / AS_SEG;
@@ -1060,6 +1337,34 @@ int launch_agg_stream(float* vol, const uint32_t* arms, const int32_t* ws, int h
         return n > 0 ? n : 256;
     }();
     const int G = S.nl < ncu ? S.nl : ncu;
+    // fused pairs: the role-split v6 (368 vs 377 us on config B); single passes: v5 (286 vs
+    // 316 us).  TSM_AGG_KERNEL=stream forces v5, =split v6 for both.
+    static const int pick = [] {
+        const char* e = getenv("TSM_AGG_KERNEL");
+        return !e ? 0 : (e[0] == 's' && e[1] == 't') ? 1 : (e[0] == 's' && e[1] == 'p') ? 2 : 0;
+    }();
+    const bool split = pick == 2 || (pick == 0 && fused);
+    if (split && agg_split_lds(P) <= 160 * 1024) {
+        static bool split_attr = false;
+        if (!split_attr) {
+            (void)hipFuncSetAttribute((const void*)k_agg_split<false, 0>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+            (void)hipFuncSetAttribute((const void*)k_agg_split<false, 49>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+            (void)hipFuncSetAttribute((const void*)k_agg_split<true, 0>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+            (void)hipFuncSetAttribute((const void*)k_agg_split<true, 49>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+            split_attr = true;
+        }
+        const size_t slds = agg_split_lds(P);
+        const dim3 sgrid(G), sblock(AX_THREADS);
+        if (fused) {
+            if (Q == 49) hipLaunchKernelGGL((k_agg_split<true, 49>), sgrid, sblock, slds, st, S, P);
+            else hipLaunchKernelGGL((k_agg_split<true, 0>), sgrid, sblock, slds, st, S, P);
+        } else {
+            if (Q == 49) hipLaunchKernelGGL((k_agg_split<false, 49>), sgrid, sblock, slds, st, S, P);
+            else hipLaunchKernelGGL((k_agg_split<false, 0>), sgrid, sblock, slds, st, S, P);
+        }
+        trace_point(fused ? "k_agg_split<fused>" : "k_agg_split", st);
+        return 0;
+    }
     const dim3 grid(G), block(AS_THREADS);
     if (fused) {
         if (Q == 49) hipLaunchKernelGGL((k_agg_stream<true, 49>), grid, block, lds, st, S, P);

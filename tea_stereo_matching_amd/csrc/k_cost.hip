@@ -12,6 +12,7 @@
 // The AD-Census cost 2 - exp(-ad/lambdaAD) - exp(-census/lambdaCensus) (:518) is
 // evaluated through two host-built tables (glibc expf on the exact arguments the
 // reference feeds to std::exp), so the device result is bit-identical.
+#include <utility>
 #include <algorithm>
 #include <stdlib.h>
 
@@ -184,6 +185,9 @@ __global__ void k_census_desc(const uint32_t* __restrict__ img, uint32_t* __rest
 // cell is 6 x (and, and_or, bcnt) + one v_sad_u8 + two LDS table reads; no descriptor
 // ever goes through LDS.  Census and AD are symmetric in (left, right), so both views
 // run the same arithmetic.
+struct F3 {  // 12-B store (global_store_dwordx3; an ext_vector of 3 would claim 16-B alignment)
+    float a, b, c;
+};
 constexpr int CW_THREADS = 256;   // 4 independent waves per workgroup (tables shared)
 constexpr int CW_LUTB = 192;      // lutB slot (188 used); padding entries follow it
 constexpr int CW_CHUNK = 16;      // staging granule: 16 records x 64 B = one LDS-DMA per wave
@@ -223,7 +227,7 @@ __device__ unsigned long long g_stamps[65536 * 8];
 enum { CW_BOTH = 0, CW_VIEW0 = 1, CW_VIEW1 = 2, CW_SHEAR = 3 };
 
 template <int E, bool HSI, bool MASK, int MODE>
-__global__ __launch_bounds__(CW_THREADS) void k_cost_walk(
+__global__ __launch_bounds__(CW_THREADS) __attribute__((amdgpu_waves_per_eu(E == 3 ? 4 : 1))) void k_cost_walk(
     const uint32_t* __restrict__ desc, const float* __restrict__ lutA, int lutA_n,
     const float* __restrict__ lutB, float* __restrict__ vol, DevParams Pk, int seg_len, int nseg,
     uint32_t* __restrict__ ctr, uint32_t ctr_base) {
@@ -290,7 +294,9 @@ __global__ __launch_bounds__(CW_THREADS) void k_cost_walk(
     // (global_load_lds_dwordx4: lane i's 16 bytes land at chunk base + 16 i, i.e. record
     // i/4, quarter i%4; no staging registers): per step they are broadcast LDS reads,
     // never an L2/HBM round trip.
-    const int slots = cost_stage_slots(seg_len + (SHEAR ? 2 * E : 0), E);
+    // steps run in groups of G (F/Fn double-buffering needs an even group)
+    constexpr int G = (E & 1) ? 2 * E : E;
+    const int slots = cost_stage_slots(seg_len + (SHEAR ? 2 * E : 0), G);
     u32x4* stF = smem_stage + (size_t)wave * 2 * slots * 4;
     u32x4* stE = stF + (size_t)slots * 4;
     const int rq = lane & 3, rr = lane >> 2;  // this lane's quarter / record of a chunk
@@ -360,11 +366,12 @@ __global__ __launch_bounds__(CW_THREADS) void k_cost_walk(
     float* o1row = vol + ((size_t)H + y) * W * Lp;  // view-1 row (SHEAR)
     load_staged(stF, 0, FA);
 
-    // one step at rotation R
-    auto step = [&](auto Rc, bool fast, int t) {  // fast: interior group, no border tests
-        constexpr int R = decltype(Rc)::value;
-        uint32_t(&F)[NW] = (R & 1) ? FB : FA;
-        uint32_t(&Fn)[NW] = (R & 1) ? FA : FB;
+    // step S of a group: rotation R = S mod E, fixed-record buffer by the parity of S
+    auto step = [&](auto Sc, bool fast, int t) {  // fast: interior group, no border tests
+        constexpr int S = decltype(Sc)::value;
+        constexpr int R = S % E;
+        uint32_t(&F)[NW] = (S & 1) ? FB : FA;
+        uint32_t(&Fn)[NW] = (S & 1) ? FA : FB;
         const int j = j0 + t;
         // the next step's records (steps past the segment end run on clamped records
         // and store nothing: no branches)
@@ -440,6 +447,13 @@ __global__ __launch_bounds__(CW_THREADS) void k_cost_walk(
 #else
         if (own) {
 #endif
+            if constexpr (E == 3) {  // labels 3l .. 3l+2: one 12-B store per lane, 768 B a pixel
+                F3 o3;
+                o3.a = c[0];
+                o3.b = c[1];
+                o3.c = c[2];
+                *reinterpret_cast<F3*>(orow + (size_t)j * Lp) = o3;
+            }
 #pragma unroll
             for (int q = 0; q < E / 4; ++q)
                 if (E * lane + 4 * q < Lp)
@@ -480,18 +494,11 @@ __global__ __launch_bounds__(CW_THREADS) void k_cost_walk(
     const int tf_hi = min(jhi - j0, count - 1);
     const bool rows_ok = !MASK && !rowOut;
     CW_STAMP(2);
-    for (int t = 0; t < count; t += E) {
-        const bool fast = rows_ok && t >= tf_lo && t + E - 1 <= tf_hi;
-        step(IC<0>{}, fast, t);
-        step(IC<1>{}, fast, t + 1);
-        step(IC<2>{}, fast, t + 2);
-        step(IC<3>{}, fast, t + 3);
-        if constexpr (E == 8) {
-            step(IC<4>{}, fast, t + 4);
-            step(IC<5>{}, fast, t + 5);
-            step(IC<6>{}, fast, t + 6);
-            step(IC<7>{}, fast, t + 7);
-        }
+    for (int t = 0; t < count; t += G) {
+        const bool fast = rows_ok && t >= tf_lo && t + G - 1 <= tf_hi;
+        [&]<int... Ss>(std::integer_sequence<int, Ss...>) {
+            (step(IC<Ss>{}, fast, t + Ss), ...);
+        }(std::make_integer_sequence<int, G>{});
     }
     };
     if constexpr (MODE == CW_VIEW0 || MODE == CW_SHEAR) {
@@ -501,6 +508,46 @@ __global__ __launch_bounds__(CW_THREADS) void k_cost_walk(
     } else {
         if (v == 0) walk(IC<0>{});
         else walk(IC<1>{});
+    }
+    // E = 3 covers labels 0..191; labels 192..Lp-1 (label 192 real at L = 193, the rest
+    // +inf padding) are the tail float4 of each pixel vector: lane l computes pixel
+    // x_lo + l of the unit from global records (one gather per unit, L2-resident)
+    if constexpr (E == 3) {
+        if (Lp > 192 && lane < count0) {
+            const int k = 192;
+            const int j = x_lo + lane;
+            uint32_t Fr[NW], Vr[NW];
+            const u32x4* rf = reinterpret_cast<const u32x4*>(dF + (size_t)clampx(j + foff) * 16);
+            const u32x4* rv = reinterpret_cast<const u32x4*>(dV + (size_t)clampx(v == 0 ? j - k : j + k) * 16);
+            pick(rf[0], rf[1], rf[2], rf[3], Fr);
+            pick(rv[0], rv[1], rv[2], rv[3], Vr);
+            uint32_t cen = 0;
+            if (!HSI) {
+#pragma unroll
+                for (int w = 0; w < 6; ++w) cen = bcnt_acc((Fr[w] & Vr[6 + w]) | (Fr[6 + w] & Vr[w]), cen);
+            } else {
+                cen = __builtin_popcount(~(Fr[0] & Vr[0])) + __builtin_popcount(~(Fr[1] & Vr[1]) & vmask_hi);
+#pragma unroll
+                for (int w = 2; w < 6; ++w) cen += __builtin_popcount((Fr[w] & Vr[4 + w]) | (Fr[4 + w] & Vr[w]));
+            }
+            const uint32_t vc = Vr[NW - 1], fc = Fr[NW - 1];
+            int ai;
+            if (!HSI) {
+                ai = (int)__builtin_amdgcn_sad_u8(fc, vc, 0u);
+            } else {
+                const int hd = (int)__builtin_amdgcn_sad_u8(fc & 0xffu, vc & 0xffu, 0u);
+                ai = 2 * min(hd, 255 - hd) + 5 * (int)__builtin_amdgcn_sad_u8(fc & 0xffff00u, vc & 0xffff00u, 0u);
+            }
+            float c = 2.f - sA[ai] - sB[cen];
+            const int xf = j + foff;
+            const bool fixed_ok = !rowOut && xf - hw >= 0 && xf + hw < W;
+            const int klo = v == 0 ? j - (W - 1 - hw) : hw - j;
+            const int khi = v == 0 ? j - hw : W - 1 - hw - j;
+            c = (fixed_ok && k >= klo && k <= khi) || k >= L ? c : 2.f;
+            if (k >= L) c = __int_as_float(0x7f800000);
+            const float inf = __int_as_float(0x7f800000);
+            *reinterpret_cast<f32x4*>(vol + (((size_t)v * H + y) * W + j) * Lp + 192) = f32x4{c, inf, inf, inf};
+        }
     }
     CW_STAMP(3);
 }
@@ -552,6 +599,7 @@ static int cost_seg_len(const DevParams& P) {
 }
 
 size_t cost_volume_lds_bytes(const DevParams& P, int lutA_n) {
+    // sized for E = 4 with the shear's margin: covers every E / group size the walk uses
     (void)P;
     (void)lutA_n;  // the tables are static LDS; this is the dynamic ring part
     const int E = P.Lp <= 256 ? 4 : 8;
@@ -646,8 +694,15 @@ int launch_cost_volume(const uint32_t* img, const uint32_t* desc, const float* l
         else launch_cost_t<4, false, false, CW_SHEAR>(desc, lutA, lutA_n, lutB, vol, P, ctr, ctr_base, st);
         return 0;
     }
-    // one wave holds the whole label axis: E labels per lane
-    if (P.Lp <= 256) { CASE(4) }
+    // one wave holds the whole label axis: E labels per lane.  At Lp 192 / 196 three labels
+    // a lane fill all 64 lanes (E = 4 would leave 15 of them idle) and a per-unit tail pass
+    // writes labels 192..195.  TSM_COST_E4=1 keeps E = 4.
+    static const bool e4 = [] {
+        const char* e = getenv("TSM_COST_E4");
+        return e && e[0] == '1';
+    }();
+    if (!e4 && !P.mask && (P.Lp == 192 || P.Lp == 196)) { CASE(3) }
+    else if (P.Lp <= 256) { CASE(4) }
     else if (P.Lp <= 512) { CASE(8) }
     else return -1;
 #undef CASE

@@ -21,6 +21,7 @@ constexpr int kWave = 64;
 // type defeats SROA in arrays and spills them to scratch)
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
 
 // POD kernel parameters (ADCensusParams, stereo_utils.h:209-244, plus geometry).
 struct DevParams {

@@ -36,8 +36,9 @@ size_t agg_lds_bytes(const DevParams& P);
 // next).  Returns -1 if the geometry does not fit.
 int launch_agg_pass(float* vol, const uint32_t* arms, const int32_t* ws, int horizontal, bool fused,
                     const DevParams& P, hipStream_t st);
-int launch_agg_stream(float* vol, const uint32_t* arms, const int32_t* ws, int horizontal, bool fused,
-                      const DevParams& P, hipStream_t st);
+// ws_base: the window-size workspace (ws, reciprocals, packed descriptors; k_window_sizes)
+int launch_agg_stream(float* vol, const uint32_t* arms, const int32_t* ws, const int32_t* ws_base,
+                      int horizontal, bool fused, const DevParams& P, hipStream_t st);
 int launch_agg_line(float* vol, const uint32_t* arms, const int32_t* ws, int horizontal,
                     const DevParams& P, hipStream_t st);
 

@@ -84,6 +84,28 @@ def test_stages_bit_exact_synthetic(matcher, tsm, oracle, case):
     assert np.array_equal(d_g, d_o)
 
 
+WIDE = [
+    # (seed, H, W, minD, maxD, model): the three-labels-a-lane walk (Lp 192 / 196) and its
+    # tail float4 (labels 192..195), both views, RGB and HSI
+    (31, 24, 300, 0, 192, 0),
+    (32, 20, 270, 0, 191, 0),
+    (33, 20, 270, 0, 188, 0),
+    (34, 22, 290, 0, 192, 1),
+    (35, 18, 260, 3, 195, 0),
+]
+
+
+@pytest.mark.parametrize("case", WIDE, ids=[f"s{c[0]}_{c[1]}x{c[2]}_d{c[3]}-{c[4]}_m{c[5]}" for c in WIDE])
+def test_cost_volume_full_label_width(matcher, tsm, oracle, case):
+    seed, H, W, mn, mx, model = case
+    left, right = _synthetic(tsm, seed, H, W, mx - mn + 1)
+    st = ("cost_init", "cost_agg")
+    d_g, g = _gpu(matcher, tsm, left, right, model, mn, mx, st)
+    d_o, o = oracle.compute(left, right, _oracle_params(oracle, model, mn, mx), st)
+    _assert_stages_equal(g, o, st)
+    assert np.array_equal(d_g, d_o)
+
+
 def test_stages_bit_exact_demo_crop(matcher, tsm, oracle, demo_pair_0600):
     l, r = demo_pair_0600
     left, right = l[300:428, 400:656].copy(), r[300:428, 400:656].copy()

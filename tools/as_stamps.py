@@ -25,5 +25,5 @@ st = st[used]
 print("blocks", st.shape[0])
 for w in (0, 3, 7, 8, 11, 15):
     a = st[:, w, :]
-    name = f"sum wave {w}" if w < 8 else f"loader {w-8}"
+    name = f"A wave {w}" if w < 8 else f"B wave {w-8}"
     print(f"{name:12s} barrier {a[:,0].mean():9.0f}  A/land {a[:,1].mean():9.0f}  B/issue {a[:,2].mean():9.0f}  total {a[:,3].mean():9.0f}")

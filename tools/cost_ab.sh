@@ -1,6 +1,6 @@
 #!/bin/bash
-# GPU box: cost-walk timing A/B (kernel trace, concurrency 1): per-view launches (default),
-# one launch for both views, shear.
+# GPU box: cost-walk timing A/B (kernel trace, concurrency 1): current default, E = 4,
+# per-view launches, segment lengths, shear.
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 mkdir -p gpurun_out
@@ -12,7 +12,10 @@ run() {  # name, env...
 }
 for a in "$@"; do
   case $a in
-    views) run views TSM_COST_SEG=48 ;;
+    cur) run cur TSM_COST_SEG=48 ;;
+    e4) run e4 TSM_COST_E4=1 ;;
+    views) run views TSM_COST_VIEWS=1 ;;
+    e4views) run e4views TSM_COST_VIEWS=1 TSM_COST_E4=1 ;;
     views32) run views32 TSM_COST_SEG=32 ;;
     views64) run views64 TSM_COST_SEG=64 ;;
     both) run both TSM_COST_BOTH=1 ;;
