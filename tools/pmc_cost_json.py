@@ -23,7 +23,7 @@ write = per_dispatch(sys.argv[2], "WRITE_SIZE")
 f_kib = sum(fetch) / len(fetch)
 w_kib = sum(write) / len(write)
 out = {
-    "kernel": "k_cost_walk<4,false,false> (config B: 1242x375, L=193, both views)",
+    "kernel": "k_cost_walk<3,false,false,0> (config B: 1242x375, L=193, both views, one launch)",
     "dispatches": {"fetch_pass": len(fetch), "write_pass": len(write)},
     "fetch_size_kib_raw": f_kib,
     "write_size_kib": w_kib,
