@@ -45,6 +45,7 @@ def parse():
     ap.add_argument("--max-disparity", type=int, default=192)
     ap.add_argument("--no-gather", action="store_true")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-ops", action="store_true", help="skip the f2-f4 operator leg")
     ap.add_argument("--cpu-threads", type=int, default=0)
     return ap.parse_args()
 
@@ -203,6 +204,8 @@ def main():
             "timing": f"HIP events around each cost-volume launch, {cost_n} launches, one pipeline (no co-running kernels)",
         },
     }
+    if rank == 0 and not args.no_ops:
+        line["next_rows"] = ops_leg(tsm, outs, lefts, H, W)
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         l, r, _ = tsm.synthetic.make_scene(1000, H, W, L)
         line["cpu_baseline"] = cpu_baseline(args, l, r)
@@ -214,6 +217,65 @@ def main():
         print(json.dumps(line), flush=True)
     if world > 1:
         dist.destroy_process_group()
+
+
+def ops_leg(tsm, outs, lefts, H, W, iters=50):
+    """SURVEY §8f rows f2-f4 on this pipeline's own outputs (untimed for `value`): the
+    device forms on config-B-sized buffers already in HBM, `iters` back-to-back launches
+    on the library's null stream, then one synchronize; us = wall time / iters.
+    Algorithmic bytes per call: colour map 11 B/px (disparity read by the min/max and
+    the LUT pass, 3 B written), depth 8, points 16, remap (BGR, fixed maps) 12: 6 B of
+    map, 3 B of source, 3 B written."""
+    import ctypes
+
+    import numpy as np
+    import torch
+    from tea_stereo_matching_amd import _native as Nn
+
+    lib = Nn.load()
+    dev = outs.device
+    N = H * W
+    disp = outs[0]
+    P = lambda t: ctypes.c_void_p(t.data_ptr())  # noqa: E731
+    lut = tsm.JETColorMap()
+    lutp = lut.ctypes.data_as(ctypes.c_void_p)
+    col = torch.empty((H, W, 3), dtype=torch.uint8, device=dev)
+    dep = torch.empty((H, W), dtype=torch.float32, device=dev)
+    xyz = torch.empty((H, W, 3), dtype=torch.float32, device=dev)
+    rect = torch.empty((H, W, 3), dtype=torch.uint8, device=dev)
+    # a rectification-like warp: 0.5 degree rotation about the centre, 1/32-px maps
+    yy, xx = np.mgrid[0:H, 0:W].astype(np.float32)
+    a = np.float32(np.pi / 360)
+    mx = (W / 2 + np.cos(a) * (xx - W / 2) - np.sin(a) * (yy - H / 2)).astype(np.float32)
+    my = (H / 2 + np.sin(a) * (xx - W / 2) + np.cos(a) * (yy - H / 2)).astype(np.float32)
+    ix, iy = np.rint(mx * 32).astype(np.int64), np.rint(my * 32).astype(np.int64)
+    xy = torch.from_numpy(np.stack([ix >> 5, iy >> 5], -1).astype(np.int16)).to(dev)
+    fxy = torch.from_numpy(((iy & 31) * 32 + (ix & 31)).astype(np.int16)).to(dev)
+    torch.cuda.synchronize()
+    calls = {
+        "f2_colormap": (11, lambda: lib.tsm_apply_colormap_device(P(disp), H, W, 4 * W, lutp, 0, 0.0, 0.0,
+                                                                  P(col), 3 * W, None)),
+        "f3_depth": (8, lambda: lib.tsm_reproject_to_depth_device(P(disp), H, W, 4 * W, 721.5, 0.54, P(dep),
+                                                                  4 * W, None)),
+        "f3_points": (16, lambda: lib.tsm_reproject_to_3d_device(P(disp), H, W, 4 * W, 721.5, 0.54, 609.6,
+                                                                 172.9, P(xyz), 12 * W, None)),
+        "f4_remap": (12, lambda: lib.tsm_remap_linear_fixed_device(P(lefts[0]), H, W, 3 * W, 3, P(xy), 4 * W,
+                                                                   P(fxy), 2 * W, H, W, P(rect), 3 * W, None)),
+    }
+    res = {}
+    for name, (bpp, fn) in calls.items():
+        assert fn() == 0 and lib.tsm_stream_synchronize(None) == 0  # warm-up
+        t0 = time.perf_counter()
+        for _ in range(iters):
+            fn()
+        assert lib.tsm_stream_synchronize(None) == 0
+        us = (time.perf_counter() - t0) / iters * 1e6
+        gbs = bpp * N / (us * 1e-6) / 1e9
+        res[name] = {"us": round(us, 2), "bytes_per_px": bpp, "GBps": round(gbs, 1),
+                     "frac": round(gbs / HBM_PEAK_GBS, 4)}
+    res["timing"] = (f"{iters} back-to-back launches per operator, wall clock incl. launch, "
+                     f"{W}x{H}, device buffers; one pipeline output as input")
+    return res
 
 
 if __name__ == "__main__":

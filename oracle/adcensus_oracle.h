@@ -118,6 +118,23 @@ void orc_cv_gauss3_filter2d(const uint8_t* src, uint8_t* dst, int H, int W); /* 
 void orc_jet_colormap(uint8_t lut[256][3]);
 void orc_apply_colormap(const float* disp, int H, int W, uint8_t* bgr_out);
 
+/* stereo_ops.c: the calls either side of the path.  Strides in
+ * elements for float / int16 / uint16 arrays, in bytes for u8 images. */
+void orc_apply_colormap_ex(const float* disp, int H, int W, size_t step_f, const uint8_t* lut,
+                           int use_range, float minv, float maxv, uint8_t* bgr, size_t out_step);
+void orc_reproject_depth(const float* disp, int H, int W, size_t step_f, float f, float b,
+                         float* depth, size_t out_step_f);
+void orc_reproject_3d(const float* disp, int H, int W, size_t step_f, float f, float b, float cx,
+                      float cy, float* xyz, size_t out_step_f);
+void orc_reproject_3d_q(const float* disp, int H, int W, size_t step_f, const double* Q,
+                        float* xyz, size_t out_step_f);
+void orc_remap_linear_fixed(const uint8_t* src, int sh, int sw, size_t sstep, int C,
+                            const int16_t* xy, size_t xy_step_e, const uint16_t* fxy,
+                            size_t fxy_step_e, int H, int W, uint8_t* dst, size_t dstep);
+void orc_remap_linear_float(const uint8_t* src, int sh, int sw, size_t sstep, int C,
+                            const float* mx, const float* my, size_t map_step_f, int H, int W,
+                            uint8_t* dst, size_t dstep);
+
 #ifdef __cplusplus
 }
 #endif

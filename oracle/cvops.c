@@ -218,20 +218,5 @@ void orc_jet_colormap(uint8_t lut[256][3]) {
 void orc_apply_colormap(const float* disp, int H, int W, uint8_t* bgr) {
     uint8_t lut[256][3];
     orc_jet_colormap(lut);
-    float mn = INFINITY, mx = -INFINITY;
-    const size_t n = (size_t)H * W;
-    for (size_t i = 0; i < n; ++i) {
-        float v = disp[i];
-        if (v < 0 || isinf(v)) continue;
-        mn = fminf(mn, v);
-        mx = fmaxf(mx, v);
-    }
-    for (size_t i = 0; i < n; ++i) {
-        float v = disp[i];
-        if (v < 0) { bgr[i * 3] = bgr[i * 3 + 1] = bgr[i * 3 + 2] = 0; continue; }
-        unsigned char idx = (unsigned char)(((v - mn) / (mx - mn)) * 255);
-        bgr[i * 3 + 0] = lut[idx][0];
-        bgr[i * 3 + 1] = lut[idx][1];
-        bgr[i * 3 + 2] = lut[idx][2];
-    }
+    orc_apply_colormap_ex(disp, H, W, (size_t)W, &lut[0][0], 0, 0.f, 0.f, bgr, (size_t)W * 3);
 }

@@ -74,6 +74,13 @@ def lib():
         _lib.orc_cv_median3f.argtypes = [_P, _P, ctypes.c_int, ctypes.c_int]
         _lib.orc_apply_colormap.argtypes = [_P, ctypes.c_int, ctypes.c_int, _P]
         _lib.orc_check_disparity_range.argtypes = [ctypes.c_int, ctypes.c_int]
+        _i, _z, _f = ctypes.c_int, ctypes.c_size_t, ctypes.c_float
+        _lib.orc_apply_colormap_ex.argtypes = [_P, _i, _i, _z, _P, _i, _f, _f, _P, _z]
+        _lib.orc_reproject_depth.argtypes = [_P, _i, _i, _z, _f, _f, _P, _z]
+        _lib.orc_reproject_3d.argtypes = [_P, _i, _i, _z, _f, _f, _f, _f, _P, _z]
+        _lib.orc_reproject_3d_q.argtypes = [_P, _i, _i, _z, _P, _P, _z]
+        _lib.orc_remap_linear_fixed.argtypes = [_P, _i, _i, _z, _i, _P, _z, _P, _z, _i, _i, _P, _z]
+        _lib.orc_remap_linear_float.argtypes = [_P, _i, _i, _z, _i, _P, _P, _z, _i, _i, _P, _z]
     return _lib
 
 
@@ -156,3 +163,108 @@ def median3f(src: np.ndarray) -> np.ndarray:
     out = np.zeros_like(src)
     lib().orc_cv_median3f(_ptr(src), _ptr(out), src.shape[0], src.shape[1])
     return out
+
+
+# ---- SURVEY §8f f2-f4 (oracle/stereo_ops.c) ---------------------------------------
+
+def apply_colormap_ex(disp: np.ndarray, lut: np.ndarray | None = None, min_val=None, max_val=None) -> np.ndarray:
+    """applyColorMap, stereo.cpp:94-118 (auto range) / :120-134 (min_val, max_val given)."""
+    disp = np.ascontiguousarray(disp, dtype=np.float32)
+    H, W = disp.shape
+    lut = jet_lut() if lut is None else np.ascontiguousarray(lut, dtype=np.uint8)
+    out = np.zeros((H, W, 3), np.uint8)
+    rng = min_val is not None
+    lib().orc_apply_colormap_ex(_ptr(disp), H, W, W, _ptr(lut), int(rng),
+                                float(min_val) if rng else 0.0, float(max_val) if rng else 0.0,
+                                _ptr(out), W * 3)
+    return out
+
+
+def reproject_to_depth(disp: np.ndarray, f: float, b: float) -> np.ndarray:
+    """reprojectToDepth, stereo.cpp:136-148."""
+    disp = np.ascontiguousarray(disp, dtype=np.float32)
+    H, W = disp.shape
+    out = np.zeros((H, W), np.float32)
+    lib().orc_reproject_depth(_ptr(disp), H, W, W, f, b, _ptr(out), W)
+    return out
+
+
+def reproject_to_3d(disp: np.ndarray, f: float, b: float, cx: float, cy: float) -> np.ndarray:
+    """reprojectTo3D(disparity, f, b, cx, cy), stereo.cpp:150-169."""
+    disp = np.ascontiguousarray(disp, dtype=np.float32)
+    H, W = disp.shape
+    out = np.zeros((H, W, 3), np.float32)
+    lib().orc_reproject_3d(_ptr(disp), H, W, W, f, b, cx, cy, _ptr(out), 3 * W)
+    return out
+
+
+def reproject_to_3d_q(disp: np.ndarray, Q: np.ndarray) -> np.ndarray:
+    """reprojectTo3D(disparity, Q), stereo.cpp:171-202 (product summed in index order)."""
+    disp = np.ascontiguousarray(disp, dtype=np.float32)
+    Q = np.ascontiguousarray(Q, dtype=np.float64).reshape(16)
+    H, W = disp.shape
+    out = np.zeros((H, W, 3), np.float32)
+    lib().orc_reproject_3d_q(_ptr(disp), H, W, W, _ptr(Q), _ptr(out), 3 * W)
+    return out
+
+
+def remap_linear_fixed(src: np.ndarray, xy: np.ndarray, fxy: np.ndarray) -> np.ndarray:
+    """cv::remap INTER_LINEAR with CV_16SC2 + CV_16UC1 maps (EpipolarRectify.cpp:99-100)."""
+    src = np.ascontiguousarray(src, dtype=np.uint8)
+    C = 1 if src.ndim == 2 else src.shape[2]
+    xy = np.ascontiguousarray(xy, dtype=np.int16)
+    fxy = np.ascontiguousarray(fxy, dtype=np.uint16)
+    H, W = fxy.shape
+    out = np.zeros((H, W, C) if C > 1 else (H, W), np.uint8)
+    lib().orc_remap_linear_fixed(_ptr(src), src.shape[0], src.shape[1], src.shape[1] * C, C,
+                                 _ptr(xy), 2 * W, _ptr(fxy), W, H, W, _ptr(out), W * C)
+    return out
+
+
+def remap_linear_float(src: np.ndarray, mapx: np.ndarray, mapy: np.ndarray) -> np.ndarray:
+    """cv::remap INTER_LINEAR with two CV_32FC1 maps."""
+    src = np.ascontiguousarray(src, dtype=np.uint8)
+    C = 1 if src.ndim == 2 else src.shape[2]
+    mapx = np.ascontiguousarray(mapx, dtype=np.float32)
+    mapy = np.ascontiguousarray(mapy, dtype=np.float32)
+    H, W = mapx.shape
+    out = np.zeros((H, W, C) if C > 1 else (H, W), np.uint8)
+    lib().orc_remap_linear_float(_ptr(src), src.shape[0], src.shape[1], src.shape[1] * C, C,
+                                 _ptr(mapx), _ptr(mapy), W, H, W, _ptr(out), W * C)
+    return out
+
+
+def _to_chars_f32(v: np.float32) -> str:
+    """std::to_chars(float) (stereo.cpp:234-238): the shortest round-trip digits, printed
+    as %f or %e, whichever is shorter (%f on a tie); exponent with at least two digits."""
+    v = np.float32(v)
+    if np.isnan(v):
+        return "-nan" if np.signbit(v) else "nan"
+    if np.isinf(v):
+        return "-inf" if v < 0 else "inf"
+    fx = np.format_float_positional(v, unique=True, trim="-")
+    sc = np.format_float_scientific(v, unique=True, trim="-", exp_digits=2)
+    return fx if len(fx) <= len(sc) else sc
+
+
+def point_cloud_text(bgr: np.ndarray, xyz: np.ndarray, kind: str) -> bytes:
+    """writePointCloudToPCD / writePointCloudToPLY (stereo.cpp:204-356): points with any
+    +inf coordinate are skipped; PCD packs rgb as r<<16 | g<<8 | b | 1<<24."""
+    pts = xyz.reshape(-1, 3)
+    col = bgr.reshape(-1, 3)
+    keep = ~(np.isposinf(pts).any(axis=1))
+    pts, col = pts[keep], col[keep]
+    n = len(pts)
+    if kind == "pcd":
+        head = ("# .PCD v0.7 - Point Cloud Data file format\nVERSION 0.7\nFIELDS x y z rgb\n"
+                "SIZE 4 4 4 4\nTYPE F F F U\nCOUNT 1 1 1 1\n"
+                f"WIDTH {n}\nHEIGHT 1\nVIEWPOINT 0 0 0 1 0 0 0\nPOINTS {n}\nDATA ascii\n")
+        lines = [f"{_to_chars_f32(p[0])} {_to_chars_f32(p[1])} {_to_chars_f32(p[2])} "
+                 f"{(int(c[2]) << 16) | (int(c[1]) << 8) | int(c[0]) | (1 << 24)}\n" for p, c in zip(pts, col)]
+    else:
+        head = ("ply\nformat ascii 1.0\n" f"element vertex {n}\n"
+                "property float x\nproperty float y\nproperty float z\n"
+                "property uchar red\nproperty uchar green\nproperty uchar blue\nend_header\n")
+        lines = [f"{_to_chars_f32(p[0])} {_to_chars_f32(p[1])} {_to_chars_f32(p[2])} "
+                 f"{int(c[2])} {int(c[1])} {int(c[0])}\n" for p, c in zip(pts, col)]
+    return (head + "".join(lines)).encode()

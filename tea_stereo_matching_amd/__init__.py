@@ -8,6 +8,9 @@ reference class plus the synthetic-pair generator used by the benchmark.
 from .adcensus import ADCensus, ADCensusError, CensusWin, ColorModel  # noqa: F401
 from ._native import LIB_PATH, device_count, version  # noqa: F401
 from . import synthetic  # noqa: F401
+from .stereo_ops import (EpipolarRectify, EpipolarRectifyMap, JETColorMap, applyColorMap,  # noqa: F401
+                         remap, reprojectTo3D, reprojectToDepth, writePointCloudToPCD,
+                         writePointCloudToPLY)
 
 __all__ = ["ADCensus", "ADCensusError", "CensusWin", "ColorModel", "LIB_PATH", "device_count",
            "version", "synthetic"]

@@ -11,6 +11,7 @@ import os
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "lib", "libtsm_adcensus.so")
 HEADER_PATH = os.path.join(os.path.dirname(_HERE), "include", "tsm_adcensus.h")
+OPS_HEADER_PATH = os.path.join(os.path.dirname(_HERE), "include", "tsm_stereo_ops.h")
 
 TSM_OK = 0
 TSM_ERR_ARGUMENT = -1
@@ -87,6 +88,27 @@ SIGNATURES = {
     "tsm_version": (ctypes.c_char_p, []),
 }
 
+_i, _z, _f = ctypes.c_int, ctypes.c_size_t, ctypes.c_float
+# every symbol include/tsm_stereo_ops.h declares
+OPS_SIGNATURES = {
+    "tsm_jet_colormap": (_i, [_P]),
+    "tsm_stream_synchronize": (_i, [_P]),
+    "tsm_apply_colormap": (_i, [_P, _i, _i, _z, _P, _i, _f, _f, _P, _z]),
+    "tsm_apply_colormap_device": (_i, [_P, _i, _i, _z, _P, _i, _f, _f, _P, _z, _P]),
+    "tsm_reproject_to_depth": (_i, [_P, _i, _i, _z, _f, _f, _P, _z]),
+    "tsm_reproject_to_depth_device": (_i, [_P, _i, _i, _z, _f, _f, _P, _z, _P]),
+    "tsm_reproject_to_3d": (_i, [_P, _i, _i, _z, _f, _f, _f, _f, _P, _z]),
+    "tsm_reproject_to_3d_device": (_i, [_P, _i, _i, _z, _f, _f, _f, _f, _P, _z, _P]),
+    "tsm_reproject_to_3d_q": (_i, [_P, _i, _i, _z, _P, _P, _z]),
+    "tsm_reproject_to_3d_q_device": (_i, [_P, _i, _i, _z, _P, _P, _z, _P]),
+    "tsm_write_point_cloud_pcd": (_i, [_P, _z, _P, _z, _i, _i, ctypes.c_char_p]),
+    "tsm_write_point_cloud_ply": (_i, [_P, _z, _P, _z, _i, _i, ctypes.c_char_p]),
+    "tsm_remap_linear_fixed": (_i, [_P, _i, _i, _z, _i, _P, _z, _P, _z, _i, _i, _P, _z]),
+    "tsm_remap_linear_fixed_device": (_i, [_P, _i, _i, _z, _i, _P, _z, _P, _z, _i, _i, _P, _z, _P]),
+    "tsm_remap_linear_float": (_i, [_P, _i, _i, _z, _i, _P, _P, _z, _i, _i, _P, _z]),
+    "tsm_remap_linear_float_device": (_i, [_P, _i, _i, _z, _i, _P, _P, _z, _i, _i, _P, _z, _P]),
+}
+
 _lib = None
 
 
@@ -101,7 +123,7 @@ def load() -> ctypes.CDLL:
             f"{path} not found: build the gfx950 library first "
             "(`make lib` or `python -c 'import __graft_entry__ as g; g.build()'`)")
     lib = ctypes.CDLL(path)
-    for name, (res, args) in SIGNATURES.items():
+    for name, (res, args) in {**SIGNATURES, **OPS_SIGNATURES}.items():
         fn = getattr(lib, name)
         fn.restype = res
         fn.argtypes = args

@@ -1,0 +1,624 @@
+// k_stereo_ops.hip -- the gfx950 operators either side of the AD-Census path (SURVEY
+// §8f f2-f4) and their C ABI (include/tsm_stereo_ops.h):
+//   f2  applyColorMap (source/stereo.cpp:94-134): a min/max pass + a LUT pass
+//   f3  reprojectToDepth / reprojectTo3D x2 (stereo.cpp:136-202): elementwise
+//   f4  cv::remap INTER_LINEAR of EpipolarRectify::rectify (EpipolarRectify.cpp:87-101)
+// All are HBM-bound streams: 4 pixels a lane along a row, so the byte-wide BGR outputs
+// leave as whole dwords (12 B a lane), and no divergent per-pixel branches beyond the
+// reference's own validity tests.
+#include <hip/hip_runtime.h>
+#include <math.h>
+#include <stdint.h>
+
+#include <map>
+#include <mutex>
+#include <utility>
+
+#include "tsm_adcensus.h"
+#include "tsm_stereo_ops.h"
+
+namespace tsm {
+namespace {
+
+constexpr int OPS_THREADS = 256;
+constexpr int OPS_PX = 4;  // pixels per lane along a row
+
+// (unsigned char)t with x86 cvttss2si semantics: NaN / out of int range -> 0x80000000
+__device__ __forceinline__ uint32_t cast_u8_x86(float t) {
+    return (t > -2147483648.0f && t < 2147483648.0f) ? ((uint32_t)(int32_t)t & 0xffu) : 0u;
+}
+
+// grid over (row, group of 4 pixels); returns false past the row end
+struct RowGrid {
+    int y, x0;
+};
+__device__ __forceinline__ RowGrid row_grid(int cols) {
+    const int groups = (cols + OPS_PX - 1) / OPS_PX;
+    const int g = blockIdx.x * blockDim.x + threadIdx.x;
+    return RowGrid{(int)blockIdx.y, g < groups ? g * OPS_PX : cols};
+}
+
+// ---- f2 ---------------------------------------------------------------------------
+
+struct Lut {
+    uint32_t bgr[256];  // b | g << 8 | r << 16
+};
+
+// min / max over pixels >= 0 and not inf (stereo.cpp:96-104).  Every such value is a
+// non-negative float (NaN is skipped as std::min/max skip it; -0.0 folds to +0.0, which
+// changes no index downstream), so the bit patterns order like the values and the
+// reduction is on integers.  Two launches: per-block partials, then one block folds them
+// into mm[0..1] (plain stores read by the next launch: no cross-XCD atomics on a word
+// other XCDs' caches may hold).
+constexpr int MM_BLOCKS = 512;
+
+__device__ __forceinline__ void block_minmax(uint32_t& lo, int& hi, uint32_t* s_lo, int* s_hi) {
+    for (int o = 32; o > 0; o >>= 1) {
+        lo = min(lo, (uint32_t)__shfl_xor((int)lo, o));
+        hi = max(hi, __shfl_xor(hi, o));
+    }
+    const int w = threadIdx.x >> 6, nw = blockDim.x >> 6;
+    if ((threadIdx.x & 63) == 0) {
+        s_lo[w] = lo;
+        s_hi[w] = hi;
+    }
+    __syncthreads();
+    lo = 0x7f800000u;
+    hi = (int)0xff800000u;
+    for (int i = 0; i < nw; ++i) {
+        lo = min(lo, s_lo[i]);
+        hi = max(hi, s_hi[i]);
+    }
+}
+
+__global__ void k_minmax(const float* __restrict__ src, int rows, int cols, size_t step_f,
+                         uint32_t* __restrict__ part) {
+    __shared__ uint32_t s_lo[16];
+    __shared__ int s_hi[16];
+    const int n = rows * cols;
+    uint32_t lo = 0x7f800000u;
+    int hi = (int)0xff800000u;  // -inf: no valid pixel
+    for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
+        const int y = i / cols, x = i - y * cols;
+        const float v = src[(size_t)y * step_f + x];
+        if (v >= 0.f && v != __int_as_float(0x7f800000)) {
+            const uint32_t b = __float_as_uint(v + 0.f);
+            lo = min(lo, b);
+            hi = max(hi, (int)b);
+        }
+    }
+    block_minmax(lo, hi, s_lo, s_hi);
+    if (threadIdx.x == 0) {
+        part[2 * blockIdx.x] = lo;
+        part[2 * blockIdx.x + 1] = (uint32_t)hi;
+    }
+}
+
+__global__ void k_minmax_final(uint32_t* __restrict__ part, int nparts, uint32_t* __restrict__ mm) {
+    __shared__ uint32_t s_lo[16];
+    __shared__ int s_hi[16];
+    uint32_t lo = 0x7f800000u;
+    int hi = (int)0xff800000u;
+    for (int i = threadIdx.x; i < nparts; i += blockDim.x) {
+        lo = min(lo, part[2 * i]);
+        hi = max(hi, (int)part[2 * i + 1]);
+    }
+    block_minmax(lo, hi, s_lo, s_hi);
+    if (threadIdx.x == 0) {
+        mm[0] = lo;
+        mm[1] = (uint32_t)hi;
+    }
+}
+
+__global__ void k_colormap(const float* __restrict__ src, int rows, int cols, size_t step_f,
+                           const uint32_t* __restrict__ mm, int use_range, float rmin, float rmax,
+                           Lut lut, uint8_t* __restrict__ dst, size_t dstep) {
+    const RowGrid p = row_grid(cols);
+    if (p.x0 >= cols) return;
+    const float mn = use_range ? rmin : __uint_as_float(mm[0]);
+    const float mx = use_range ? rmax : __int_as_float((int)mm[1]);
+    const float* s = src + (size_t)p.y * step_f;
+    uint8_t* d = dst + (size_t)p.y * dstep + 3 * (size_t)p.x0;
+    const int n = min(OPS_PX, cols - p.x0);
+    uint32_t c[OPS_PX];
+#pragma unroll
+    for (int k = 0; k < OPS_PX; ++k) {
+        const float v = k < n ? s[p.x0 + k] : 0.f;
+        const bool black = use_range ? (v < mn || v > mx) : (v < 0.f);
+        c[k] = black ? 0u : lut.bgr[cast_u8_x86(((v - mn) / (mx - mn)) * 255)];
+    }
+    if (n == OPS_PX && ((uintptr_t)d & 3) == 0) {  // 12 B: three dword stores
+        uint32_t* d4 = reinterpret_cast<uint32_t*>(d);
+        d4[0] = c[0] | (c[1] << 24);
+        d4[1] = (c[1] >> 8) | (c[2] << 16);
+        d4[2] = (c[2] >> 16) | (c[3] << 8);
+    } else {
+        for (int k = 0; k < n; ++k) {
+            d[3 * k + 0] = (uint8_t)c[k];
+            d[3 * k + 1] = (uint8_t)(c[k] >> 8);
+            d[3 * k + 2] = (uint8_t)(c[k] >> 16);
+        }
+    }
+}
+
+// ---- f3 ---------------------------------------------------------------------------
+
+__global__ void k_depth(const float* __restrict__ src, int rows, int cols, size_t step_f, float fb,
+                        float* __restrict__ dst, size_t dstep_f) {
+    const RowGrid p = row_grid(cols);
+    if (p.x0 >= cols) return;
+    const int n = min(OPS_PX, cols - p.x0);
+    for (int k = 0; k < n; ++k) {
+        const float d = src[(size_t)p.y * step_f + p.x0 + k];
+        dst[(size_t)p.y * dstep_f + p.x0 + k] = (d < 0.f || isinf(d)) ? 0.f : fb / d;
+    }
+}
+
+struct F3 {
+    float x, y, z;
+};
+
+__global__ void k_xyz(const float* __restrict__ src, int rows, int cols, size_t step_f, float f,
+                      float fb, float cx, float cy, float* __restrict__ dst, size_t dstep_f) {
+    const RowGrid p = row_grid(cols);
+    if (p.x0 >= cols) return;
+    const int n = min(OPS_PX, cols - p.x0);
+    const float v = (float)p.y;
+    for (int k = 0; k < n; ++k) {
+        const int u = p.x0 + k;
+        const float d = src[(size_t)p.y * step_f + u];
+        F3 o{0.f, 0.f, 0.f};
+        if (!(d < 0.f || isinf(d))) {
+            const float Z = fb / d;
+            const float Zf = Z / f;
+            o = F3{((float)u - cx) * Zf, (v - cy) * Zf, Z};
+        }
+        *reinterpret_cast<F3*>(dst + (size_t)p.y * dstep_f + 3 * (size_t)u) = o;
+    }
+}
+
+struct Q16 {
+    float q[16];
+};
+
+__global__ void k_xyz_q(const float* __restrict__ src, int rows, int cols, size_t step_f, Q16 Q,
+                        float* __restrict__ dst, size_t dstep_f) {
+    const RowGrid p = row_grid(cols);
+    if (p.x0 >= cols) return;
+    const int n = min(OPS_PX, cols - p.x0);
+    for (int k = 0; k < n; ++k) {
+        const int u = p.x0 + k;
+        const float pv[4] = {(float)u, (float)p.y, src[(size_t)p.y * step_f + u], 1.f};
+        float r[4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            float s = 0.f;
+#pragma unroll
+            for (int j = 0; j < 4; ++j) s += Q.q[4 * i + j] * pv[j];
+            r[i] = s;
+        }
+        *reinterpret_cast<F3*>(dst + (size_t)p.y * dstep_f + 3 * (size_t)u) =
+            F3{r[0] / r[3], r[1] / r[3], r[2] / r[3]};
+    }
+}
+
+// ---- f4 ---------------------------------------------------------------------------
+
+// One source row's two taps (2*C bytes from byte x*C): a 12-B dword window at the
+// aligned base, bytes picked by v_alignbyte; rows outside, or taps past either edge,
+// read the border value 0 byte by byte.
+template <int C>
+__device__ __forceinline__ void row_taps(const uint8_t* __restrict__ src, int sh, int sw,
+                                         size_t sstep, int sx, int sy, uint32_t (&b)[2 * C]) {
+    if (sy < 0 || sy >= sh) {
+#pragma unroll
+        for (int i = 0; i < 2 * C; ++i) b[i] = 0;
+        return;
+    }
+    const uint8_t* row = src + (size_t)sy * sstep;
+    const long off = (long)sx * C;
+    const long base = off & ~3L;
+    if (sx >= 0 && sx + 1 < sw && base + 12 <= (long)sw * C && (((uintptr_t)(row + base)) & 3) == 0) {
+        const uint32_t* w = reinterpret_cast<const uint32_t*>(row + base);
+        const uint32_t w0 = w[0], w1 = w[1], w2 = w[2];
+        const uint32_t sh8 = (uint32_t)(off & 3) * 8;
+        const uint32_t lo = __builtin_amdgcn_alignbit(w1, w0, sh8);
+        const uint32_t hi = __builtin_amdgcn_alignbit(w2, w1, sh8);
+#pragma unroll
+        for (int i = 0; i < 2 * C; ++i) b[i] = ((i < 4 ? lo : hi) >> (8 * (i & 3))) & 0xffu;
+        return;
+    }
+#pragma unroll
+    for (int t = 0; t < 2; ++t) {
+        const int x = sx + t;
+        const bool in = x >= 0 && x < sw;
+#pragma unroll
+        for (int c = 0; c < C; ++c) b[t * C + c] = in ? row[(size_t)x * C + c] : 0u;
+    }
+}
+
+template <int C>
+__device__ __forceinline__ void remap_px(const uint8_t* __restrict__ src, int sh, int sw, size_t sstep,
+                                         int sx, int sy, int fx, int fy, uint32_t (&o)[C]) {
+    const uint32_t w00 = (uint32_t)((32 - fx) * (32 - fy) * 32), w01 = (uint32_t)(fx * (32 - fy) * 32);
+    const uint32_t w10 = (uint32_t)((32 - fx) * fy * 32), w11 = (uint32_t)(fx * fy * 32);
+    uint32_t t0[2 * C], t1[2 * C];
+    row_taps<C>(src, sh, sw, sstep, sx, sy, t0);
+    row_taps<C>(src, sh, sw, sstep, sx, sy + 1, t1);
+#pragma unroll
+    for (int c = 0; c < C; ++c)
+        o[c] = (t0[c] * w00 + t0[C + c] * w01 + t1[c] * w10 + t1[C + c] * w11 + (1u << 14)) >> 15;
+}
+
+template <int C>
+__device__ __forceinline__ void store_px(uint8_t* d, int n, const uint32_t (&o)[OPS_PX][C]) {
+    uint8_t bytes[OPS_PX * C];
+#pragma unroll
+    for (int k = 0; k < OPS_PX; ++k)
+#pragma unroll
+        for (int c = 0; c < C; ++c) bytes[k * C + c] = (uint8_t)o[k][c];
+    if (n == OPS_PX && ((uintptr_t)d & 3) == 0) {  // 4*C bytes as C dwords
+        uint32_t* d4 = reinterpret_cast<uint32_t*>(d);
+#pragma unroll
+        for (int i = 0; i < C; ++i)
+            d4[i] = (uint32_t)bytes[4 * i] | ((uint32_t)bytes[4 * i + 1] << 8) |
+                    ((uint32_t)bytes[4 * i + 2] << 16) | ((uint32_t)bytes[4 * i + 3] << 24);
+    } else {
+        for (int i = 0; i < n * C; ++i) d[i] = bytes[i];
+    }
+}
+
+template <int C>
+__global__ void k_remap_fixed(const uint8_t* __restrict__ src, int sh, int sw, size_t sstep,
+                              const int16_t* __restrict__ xy, size_t xy_step_e,
+                              const uint16_t* __restrict__ fxy, size_t fxy_step_e, int rows, int cols,
+                              uint8_t* __restrict__ dst, size_t dstep) {
+    const RowGrid p = row_grid(cols);
+    if (p.x0 >= cols) return;
+    const int n = min(OPS_PX, cols - p.x0);
+    uint32_t o[OPS_PX][C];
+#pragma unroll
+    for (int k = 0; k < OPS_PX; ++k) {
+        const int x = min(p.x0 + k, cols - 1);
+        const int sx = xy[(size_t)p.y * xy_step_e + 2 * (size_t)x];
+        const int sy = xy[(size_t)p.y * xy_step_e + 2 * (size_t)x + 1];
+        const int f = fxy[(size_t)p.y * fxy_step_e + x] & 1023;
+        remap_px<C>(src, sh, sw, sstep, sx, sy, f & 31, f >> 5, o[k]);
+    }
+    store_px<C>(dst + (size_t)p.y * dstep + (size_t)p.x0 * C, n, o);
+}
+
+// saturate_cast<int>(v * 32) = cvRound, x86: nearest-even, NaN / out of range -> INT_MIN
+__device__ __forceinline__ int round32(float v) {
+    const float a = v * 32.f;
+    return (a >= -2147483648.0f && a < 2147483648.0f) ? (int)rintf(a) : (int)0x80000000u;
+}
+
+template <int C>
+__global__ void k_remap_float(const uint8_t* __restrict__ src, int sh, int sw, size_t sstep,
+                              const float* __restrict__ mapx, const float* __restrict__ mapy,
+                              size_t map_step_f, int rows, int cols, uint8_t* __restrict__ dst,
+                              size_t dstep) {
+    const RowGrid p = row_grid(cols);
+    if (p.x0 >= cols) return;
+    const int n = min(OPS_PX, cols - p.x0);
+    uint32_t o[OPS_PX][C];
+#pragma unroll
+    for (int k = 0; k < OPS_PX; ++k) {
+        const int x = min(p.x0 + k, cols - 1);
+        const int ix = round32(mapx[(size_t)p.y * map_step_f + x]);
+        const int iy = round32(mapy[(size_t)p.y * map_step_f + x]);
+        const int sx = min(max(ix >> 5, -32768), 32767), sy = min(max(iy >> 5, -32768), 32767);
+        remap_px<C>(src, sh, sw, sstep, sx, sy, ix & 31, iy & 31, o[k]);
+    }
+    store_px<C>(dst + (size_t)p.y * dstep + (size_t)p.x0 * C, n, o);
+}
+
+// ---- host side --------------------------------------------------------------------
+
+dim3 row_blocks(int rows, int cols) {
+    const int groups = (cols + OPS_PX - 1) / OPS_PX;
+    return dim3((groups + OPS_THREADS - 1) / OPS_THREADS, rows);
+}
+
+bool bad_dims(int rows, int cols) { return rows <= 0 || cols <= 0; }
+
+Lut make_lut(const uint8_t* lut768) {
+    uint8_t jet[768];
+    if (!lut768) {
+        tsm_jet_colormap(jet);
+        lut768 = jet;
+    }
+    Lut L;
+    for (int i = 0; i < 256; ++i)
+        L.bgr[i] = lut768[3 * i] | ((uint32_t)lut768[3 * i + 1] << 8) | ((uint32_t)lut768[3 * i + 2] << 16);
+    return L;
+}
+
+// RAII device buffer for the host forms
+struct DevBuf {
+    void* p = nullptr;
+    hipError_t e = hipSuccess;
+    explicit DevBuf(size_t n) { e = hipMalloc(&p, n ? n : 1); }
+    ~DevBuf() { if (p) (void)hipFree(p); }
+};
+
+int status(hipError_t e) {
+    if (e == hipSuccess) return TSM_OK;
+    return e == hipErrorOutOfMemory || e == hipErrorMemoryAllocation ? TSM_ERR_OUT_OF_MEMORY : TSM_ERR_DEVICE;
+}
+
+int device_ok() {
+    int n = 0;
+    return hipGetDeviceCount(&n) == hipSuccess && n > 0;
+}
+
+// host form helper: upload `in` (rows of in_row bytes at in_step), run `op` on the dense
+// device copies, download `out` rows of out_row bytes to out_step
+template <class Op>
+int host_form(const void* in, size_t in_row, size_t in_step, int rows, void* out, size_t out_row,
+              size_t out_step, Op op) {
+    if (!device_ok()) return TSM_ERR_DEVICE;
+    DevBuf di(in_row * rows), dout(out_row * rows);
+    if (di.e != hipSuccess) return status(di.e);
+    if (dout.e != hipSuccess) return status(dout.e);
+    hipError_t e = hipMemcpy2D(di.p, in_row, in, in_step, in_row, rows, hipMemcpyHostToDevice);
+    if (e != hipSuccess) return status(e);
+    int rc = op(di.p, in_row, dout.p, out_row);
+    if (rc != TSM_OK) return rc;
+    e = hipMemcpy2D(out, out_step, dout.p, out_row, out_row, rows, hipMemcpyDeviceToHost);
+    return status(e);
+}
+
+
+constexpr size_t MM_SCRATCH_BYTES = (size_t)(2 * MM_BLOCKS + 2) * 4;
+
+// the min/max scratch of the _device form: one buffer per (device, stream), kept for the
+// process lifetime (launches on one stream are ordered, so reuse is safe)
+uint32_t* stream_scratch(void* stream) {
+    static std::mutex mu;
+    static std::map<std::pair<int, void*>, void*> bufs;
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess) return nullptr;
+    std::lock_guard<std::mutex> lk(mu);
+    void*& p = bufs[{dev, stream}];
+    if (!p && hipMalloc(&p, MM_SCRATCH_BYTES) != hipSuccess) p = nullptr;
+    return (uint32_t*)p;
+}
+
+int colormap_launch(const float* d_disp, int rows, int cols, size_t step, const uint8_t* lut768, int use_range,
+                    float min_val, float max_val, uint8_t* d_bgr, size_t out_step, uint32_t* scratch,
+                    hipStream_t st) {
+    const Lut L = make_lut(lut768);
+    uint32_t* mm = scratch;  // [0..1] folded min / max, then MM_BLOCKS partial pairs
+    if (!use_range) {
+        const int n = rows * cols;
+        const int blocks = min((n + OPS_THREADS - 1) / OPS_THREADS, MM_BLOCKS);
+        hipLaunchKernelGGL(k_minmax, dim3(blocks), dim3(OPS_THREADS), 0, st, d_disp, rows, cols, step / 4, mm + 2);
+        hipLaunchKernelGGL(k_minmax_final, dim3(1), dim3(1024), 0, st, mm + 2, blocks, mm);
+    }
+    hipLaunchKernelGGL(k_colormap, row_blocks(rows, cols), dim3(OPS_THREADS), 0, st, d_disp, rows, cols,
+                       step / 4, mm, use_range, min_val, max_val, L, d_bgr, out_step);
+    return status(hipGetLastError());
+}
+
+}  // namespace
+}  // namespace tsm
+
+using namespace tsm;
+
+extern "C" {
+
+int tsm_stream_synchronize(void* hip_stream) {
+    return status(hipStreamSynchronize((hipStream_t)hip_stream));
+}
+
+int tsm_jet_colormap(uint8_t* lut) {
+    if (!lut) return TSM_ERR_ARGUMENT;
+    auto set = [&](int i, int b, int g, int r) {
+        lut[3 * i] = (uint8_t)b;
+        lut[3 * i + 1] = (uint8_t)g;
+        lut[3 * i + 2] = (uint8_t)r;
+    };
+    for (int i = 0; i < 32; ++i) set(i, 128 + 4 * i, 0, 0);
+    set(32, 255, 0, 0);
+    for (int i = 0; i < 63; ++i) set(33 + i, 255, 4 + 4 * i, 0);
+    set(96, 254, 255, 2);
+    for (int i = 0; i < 62; ++i) set(97 + i, 250 - 4 * i, 255, 6 + 4 * i);
+    set(159, 1, 255, 254);
+    for (int i = 0; i < 64; ++i) set(160 + i, 0, 252 - 4 * i, 255);
+    for (int i = 0; i < 32; ++i) set(224 + i, 0, 0, 252 - 4 * i);
+    return TSM_OK;
+}
+
+int tsm_apply_colormap_device(const float* d_disp, int rows, int cols, size_t step, const uint8_t* lut768,
+                              int use_range, float min_val, float max_val, uint8_t* d_bgr,
+                              size_t out_step, void* hip_stream) {
+    if (!d_disp || !d_bgr || bad_dims(rows, cols) || step % 4 || step < 4 * (size_t)cols ||
+        out_step < 3 * (size_t)cols)
+        return TSM_ERR_ARGUMENT;
+    uint32_t* scratch = nullptr;
+    if (!use_range) {
+        scratch = stream_scratch(hip_stream);
+        if (!scratch) return TSM_ERR_OUT_OF_MEMORY;
+    }
+    return colormap_launch(d_disp, rows, cols, step, lut768, use_range, min_val, max_val, d_bgr, out_step,
+                           scratch, (hipStream_t)hip_stream);
+}
+
+int tsm_apply_colormap(const float* disp, int rows, int cols, size_t step, const uint8_t* lut768,
+                       int use_range, float min_val, float max_val, uint8_t* bgr, size_t out_step) {
+    if (!disp || !bgr || bad_dims(rows, cols) || step < 4 * (size_t)cols || out_step < 3 * (size_t)cols)
+        return TSM_ERR_ARGUMENT;
+    if (!device_ok()) return TSM_ERR_DEVICE;
+    DevBuf scratch(MM_SCRATCH_BYTES);
+    if (scratch.e != hipSuccess) return status(scratch.e);
+    return host_form(disp, 4 * (size_t)cols, step, rows, bgr, 3 * (size_t)cols, out_step,
+                     [&](void* di, size_t is, void* dout, size_t os) {
+                         int rc = colormap_launch((const float*)di, rows, cols, is, lut768, use_range, min_val,
+                                                  max_val, (uint8_t*)dout, os, (uint32_t*)scratch.p, nullptr);
+                         return rc != TSM_OK ? rc : status(hipDeviceSynchronize());
+                     });
+}
+
+int tsm_reproject_to_depth_device(const float* d_disp, int rows, int cols, size_t step, float focal,
+                                  float baseline, float* d_depth, size_t out_step, void* hip_stream) {
+    if (!d_disp || !d_depth || bad_dims(rows, cols) || step % 4 || out_step % 4 ||
+        step < 4 * (size_t)cols || out_step < 4 * (size_t)cols)
+        return TSM_ERR_ARGUMENT;
+    hipLaunchKernelGGL(k_depth, row_blocks(rows, cols), dim3(OPS_THREADS), 0, (hipStream_t)hip_stream,
+                       d_disp, rows, cols, step / 4, focal * baseline, d_depth, out_step / 4);
+    return status(hipGetLastError());
+}
+
+int tsm_reproject_to_depth(const float* disp, int rows, int cols, size_t step, float focal,
+                           float baseline, float* depth, size_t out_step) {
+    if (!disp || !depth || bad_dims(rows, cols) || step < 4 * (size_t)cols || out_step < 4 * (size_t)cols)
+        return TSM_ERR_ARGUMENT;
+    return host_form(disp, 4 * (size_t)cols, step, rows, depth, 4 * (size_t)cols, out_step,
+                     [&](void* di, size_t is, void* dout, size_t os) {
+                         int rc = tsm_reproject_to_depth_device((const float*)di, rows, cols, is, focal,
+                                                                baseline, (float*)dout, os, nullptr);
+                         return rc != TSM_OK ? rc : status(hipDeviceSynchronize());
+                     });
+}
+
+int tsm_reproject_to_3d_device(const float* d_disp, int rows, int cols, size_t step, float focal,
+                               float baseline, float cx, float cy, float* d_xyz, size_t out_step,
+                               void* hip_stream) {
+    if (!d_disp || !d_xyz || bad_dims(rows, cols) || step % 4 || out_step % 4 ||
+        step < 4 * (size_t)cols || out_step < 12 * (size_t)cols)
+        return TSM_ERR_ARGUMENT;
+    hipLaunchKernelGGL(k_xyz, row_blocks(rows, cols), dim3(OPS_THREADS), 0, (hipStream_t)hip_stream,
+                       d_disp, rows, cols, step / 4, focal, focal * baseline, cx, cy, d_xyz, out_step / 4);
+    return status(hipGetLastError());
+}
+
+int tsm_reproject_to_3d(const float* disp, int rows, int cols, size_t step, float focal,
+                        float baseline, float cx, float cy, float* xyz, size_t out_step) {
+    if (!disp || !xyz || bad_dims(rows, cols) || step < 4 * (size_t)cols || out_step < 12 * (size_t)cols)
+        return TSM_ERR_ARGUMENT;
+    return host_form(disp, 4 * (size_t)cols, step, rows, xyz, 12 * (size_t)cols, out_step,
+                     [&](void* di, size_t is, void* dout, size_t os) {
+                         int rc = tsm_reproject_to_3d_device((const float*)di, rows, cols, is, focal, baseline,
+                                                             cx, cy, (float*)dout, os, nullptr);
+                         return rc != TSM_OK ? rc : status(hipDeviceSynchronize());
+                     });
+}
+
+int tsm_reproject_to_3d_q_device(const float* d_disp, int rows, int cols, size_t step,
+                                 const double* q16, float* d_xyz, size_t out_step, void* hip_stream) {
+    if (!d_disp || !d_xyz || !q16 || bad_dims(rows, cols) || step % 4 || out_step % 4 ||
+        step < 4 * (size_t)cols || out_step < 12 * (size_t)cols)
+        return TSM_ERR_ARGUMENT;
+    Q16 Q;
+    for (int i = 0; i < 16; ++i) Q.q[i] = (float)q16[i];  // Q.convertTo(CV_32F), stereo.cpp:190
+    hipLaunchKernelGGL(k_xyz_q, row_blocks(rows, cols), dim3(OPS_THREADS), 0, (hipStream_t)hip_stream,
+                       d_disp, rows, cols, step / 4, Q, d_xyz, out_step / 4);
+    return status(hipGetLastError());
+}
+
+int tsm_reproject_to_3d_q(const float* disp, int rows, int cols, size_t step, const double* q16,
+                          float* xyz, size_t out_step) {
+    if (!disp || !xyz || !q16 || bad_dims(rows, cols) || step < 4 * (size_t)cols || out_step < 12 * (size_t)cols)
+        return TSM_ERR_ARGUMENT;
+    return host_form(disp, 4 * (size_t)cols, step, rows, xyz, 12 * (size_t)cols, out_step,
+                     [&](void* di, size_t is, void* dout, size_t os) {
+                         int rc = tsm_reproject_to_3d_q_device((const float*)di, rows, cols, is, q16,
+                                                               (float*)dout, os, nullptr);
+                         return rc != TSM_OK ? rc : status(hipDeviceSynchronize());
+                     });
+}
+
+int tsm_remap_linear_fixed_device(const uint8_t* d_src, int src_rows, int src_cols, size_t src_step,
+                                  int channels, const int16_t* d_xy, size_t xy_step,
+                                  const uint16_t* d_fxy, size_t fxy_step, int rows, int cols,
+                                  uint8_t* d_dst, size_t dst_step, void* hip_stream) {
+    const int C = channels;
+    if (!d_src || !d_xy || !d_fxy || !d_dst || bad_dims(rows, cols) || bad_dims(src_rows, src_cols) ||
+        (C != 1 && C != 3 && C != 4) || src_step < (size_t)C * src_cols || xy_step % 2 || fxy_step % 2 ||
+        xy_step < 4 * (size_t)cols || fxy_step < 2 * (size_t)cols || dst_step < (size_t)C * cols)
+        return TSM_ERR_ARGUMENT;
+    hipStream_t st = (hipStream_t)hip_stream;
+    const dim3 g = row_blocks(rows, cols);
+#define TSM_REMAP_FIXED(CC)                                                                       \
+    hipLaunchKernelGGL(k_remap_fixed<CC>, g, dim3(OPS_THREADS), 0, st, d_src, src_rows, src_cols, \
+                       src_step, d_xy, xy_step / 2, d_fxy, fxy_step / 2, rows, cols, d_dst, dst_step)
+    if (C == 1) TSM_REMAP_FIXED(1);
+    else if (C == 3) TSM_REMAP_FIXED(3);
+    else TSM_REMAP_FIXED(4);
+#undef TSM_REMAP_FIXED
+    return status(hipGetLastError());
+}
+
+int tsm_remap_linear_float_device(const uint8_t* d_src, int src_rows, int src_cols, size_t src_step,
+                                  int channels, const float* d_mapx, const float* d_mapy,
+                                  size_t map_step, int rows, int cols, uint8_t* d_dst,
+                                  size_t dst_step, void* hip_stream) {
+    const int C = channels;
+    if (!d_src || !d_mapx || !d_mapy || !d_dst || bad_dims(rows, cols) || bad_dims(src_rows, src_cols) ||
+        (C != 1 && C != 3 && C != 4) || src_step < (size_t)C * src_cols || map_step % 4 ||
+        map_step < 4 * (size_t)cols || dst_step < (size_t)C * cols)
+        return TSM_ERR_ARGUMENT;
+    hipStream_t st = (hipStream_t)hip_stream;
+    const dim3 g = row_blocks(rows, cols);
+#define TSM_REMAP_FLOAT(CC)                                                                       \
+    hipLaunchKernelGGL(k_remap_float<CC>, g, dim3(OPS_THREADS), 0, st, d_src, src_rows, src_cols, \
+                       src_step, d_mapx, d_mapy, map_step / 4, rows, cols, d_dst, dst_step)
+    if (C == 1) TSM_REMAP_FLOAT(1);
+    else if (C == 3) TSM_REMAP_FLOAT(3);
+    else TSM_REMAP_FLOAT(4);
+#undef TSM_REMAP_FLOAT
+    return status(hipGetLastError());
+}
+
+// host forms of the remap: three inputs (image, two maps), one output
+static int remap_host(const uint8_t* src, int src_rows, int src_cols, size_t src_step, int C,
+                      const void* m1, size_t m1_row, size_t m1_step, const void* m2, size_t m2_row,
+                      size_t m2_step, int rows, int cols, uint8_t* dst, size_t dst_step, bool fixed) {
+    if (!device_ok()) return TSM_ERR_DEVICE;
+    const size_t srow = (size_t)C * src_cols, drow = (size_t)C * cols;
+    DevBuf ds(srow * src_rows), d1(m1_row * rows), d2(m2_row * rows), dd(drow * rows);
+    for (DevBuf* b : {&ds, &d1, &d2, &dd})
+        if (b->e != hipSuccess) return status(b->e);
+    hipError_t e = hipMemcpy2D(ds.p, srow, src, src_step, srow, src_rows, hipMemcpyHostToDevice);
+    if (e == hipSuccess) e = hipMemcpy2D(d1.p, m1_row, m1, m1_step, m1_row, rows, hipMemcpyHostToDevice);
+    if (e == hipSuccess) e = hipMemcpy2D(d2.p, m2_row, m2, m2_step, m2_row, rows, hipMemcpyHostToDevice);
+    if (e != hipSuccess) return status(e);
+    const int rc = fixed ? tsm_remap_linear_fixed_device((const uint8_t*)ds.p, src_rows, src_cols, srow, C,
+                                                         (const int16_t*)d1.p, m1_row, (const uint16_t*)d2.p,
+                                                         m2_row, rows, cols, (uint8_t*)dd.p, drow, nullptr)
+                         : tsm_remap_linear_float_device((const uint8_t*)ds.p, src_rows, src_cols, srow, C,
+                                                         (const float*)d1.p, (const float*)d2.p, m1_row, rows,
+                                                         cols, (uint8_t*)dd.p, drow, nullptr);
+    if (rc != TSM_OK) return rc;
+    e = hipDeviceSynchronize();
+    if (e == hipSuccess) e = hipMemcpy2D(dst, dst_step, dd.p, drow, drow, rows, hipMemcpyDeviceToHost);
+    return status(e);
+}
+
+int tsm_remap_linear_fixed(const uint8_t* src, int src_rows, int src_cols, size_t src_step,
+                           int channels, const int16_t* xy, size_t xy_step, const uint16_t* fxy,
+                           size_t fxy_step, int rows, int cols, uint8_t* dst, size_t dst_step) {
+    const int C = channels;
+    if (!src || !xy || !fxy || !dst || bad_dims(rows, cols) || bad_dims(src_rows, src_cols) ||
+        (C != 1 && C != 3 && C != 4) || src_step < (size_t)C * src_cols || xy_step < 4 * (size_t)cols ||
+        fxy_step < 2 * (size_t)cols || dst_step < (size_t)C * cols)
+        return TSM_ERR_ARGUMENT;
+    return remap_host(src, src_rows, src_cols, src_step, C, xy, 4 * (size_t)cols, xy_step, fxy,
+                      2 * (size_t)cols, fxy_step, rows, cols, dst, dst_step, true);
+}
+
+int tsm_remap_linear_float(const uint8_t* src, int src_rows, int src_cols, size_t src_step,
+                           int channels, const float* mapx, const float* mapy, size_t map_step,
+                           int rows, int cols, uint8_t* dst, size_t dst_step) {
+    const int C = channels;
+    if (!src || !mapx || !mapy || !dst || bad_dims(rows, cols) || bad_dims(src_rows, src_cols) ||
+        (C != 1 && C != 3 && C != 4) || src_step < (size_t)C * src_cols || map_step < 4 * (size_t)cols ||
+        dst_step < (size_t)C * cols)
+        return TSM_ERR_ARGUMENT;
+    return remap_host(src, src_rows, src_cols, src_step, C, mapx, 4 * (size_t)cols, map_step, mapy,
+                      4 * (size_t)cols, map_step, rows, cols, dst, dst_step, false);
+}
+
+}  // extern "C"

@@ -64,6 +64,55 @@ int main() {
     stereo::DisparityMap d2;
     sm->compute(L, R, d2);
     CHECK(d2.data == d.data);
+
+    // the calls around the matcher (stereo.cpp:75-356, EpipolarRectify.cpp), as a caller
+    // chains them: colour map, depth, points, point cloud, rectification
+    const stereo::ColorMapTable jet = stereo::JETColorMap();
+    CHECK(jet[0] == 128 && jet[1] == 0 && jet[3 * 255 + 2] == 128);
+    stereo::ColorImage vis;
+    stereo::applyColorMap(d, vis, jet);
+    CHECK(vis.rows == H && vis.cols == W && (int)vis.data.size() == H * W * 3);
+    stereo::ColorImage vis2;
+    stereo::applyColorMap(d, vis2, 0.f, 16.f, jet);
+    CHECK(vis2.data.size() == vis.data.size());
+    stereo::DisparityMap depth;
+    stereo::reprojectToDepth(d, 700.f, 0.1f, depth);
+    bool depth_ok = true;
+    for (int i = 0; i < H * W; ++i)
+        if (d.data[i] > 0 && depth.data[i] != (700.f * 0.1f) / d.data[i]) depth_ok = false;
+    CHECK(depth_ok);
+    stereo::PointImage xyz;
+    stereo::reprojectTo3D(d, 700.f, 0.1f, W / 2.f, H / 2.f, xyz);
+    CHECK(xyz.rows == H && (int)xyz.data.size() == H * W * 3);
+    CHECK(xyz.data[2 * 3 * W + 3 * 40 + 2] == depth.at(2, 40));
+    stereo::writePointCloudToPLY(L, xyz, "/tmp/tsm_cpp_api_cloud.ply");
+    FILE* f = std::fopen("/tmp/tsm_cpp_api_cloud.ply", "rb");
+    CHECK(f != nullptr);
+    if (f) {
+        char head[4] = {0};
+        CHECK(std::fread(head, 1, 3, f) == 3 && std::string(head) == "ply");
+        std::fclose(f);
+    }
+    stereo::EpipolarRectifyMap rm;  // identity maps: rectify returns its inputs
+    rm.rows = H;
+    rm.cols = W;
+    rm.map00.resize((size_t)H * W * 2);
+    for (int y = 0; y < H; ++y)
+        for (int x = 0; x < W; ++x) {
+            rm.map00[(size_t)(y * W + x) * 2] = (int16_t)x;
+            rm.map00[(size_t)(y * W + x) * 2 + 1] = (int16_t)y;
+        }
+    rm.map10 = rm.map00;
+    rm.map01.assign((size_t)H * W, 0);
+    rm.map11 = rm.map01;
+    stereo::EpipolarRectify rect(rm, stereo::Size{W, H});
+    stereo::ColorImage rl, rr;
+    rect.rectify(L, R, rl, rr);
+    CHECK(rl.data == l && rr.data == r);
+    bool threw = false;
+    try { stereo::EpipolarRectify().loadEpipolarRectifyMap(stereo::EpipolarRectifyMap{}, stereo::Size{W, H}); }
+    catch (const std::runtime_error& e) { threw = std::string(e.what()) == "stereo params is empty, please load it first"; }
+    CHECK(threw);
     std::printf("%s (%d failures)\n", fails ? "FAILED" : "OK", fails);
     return fails ? 1 : 0;
 }

@@ -12,8 +12,8 @@ import tea_stereo_matching_amd as tsm
 from tea_stereo_matching_amd import _native as N
 
 
-def declared_symbols():
-    text = open(N.HEADER_PATH).read()
+def declared_symbols(path=None):
+    text = open(path or N.HEADER_PATH).read()
     text = re.sub(r"/\*.*?\*/", "", text, flags=re.S)
     return sorted(set(re.findall(r"\b(tsm_[a-z_0-9]+)\s*\(", text)))
 
@@ -32,6 +32,24 @@ def test_library_exports_every_declared_symbol():
     assert not missing, missing
     # and the binding table covers the whole header
     assert set(declared_symbols()) == set(N.SIGNATURES)
+
+
+def test_library_exports_every_stereo_ops_symbol():
+    lib = N.load()
+    syms = declared_symbols(N.OPS_HEADER_PATH)
+    missing = [s for s in syms if not hasattr(lib, s)]
+    assert not missing, missing
+    assert set(syms) == set(N.OPS_SIGNATURES)
+
+
+def test_stereo_ops_argument_errors_without_compute():
+    lib = N.load()
+    assert lib.tsm_jet_colormap(None) == N.TSM_ERR_ARGUMENT
+    assert lib.tsm_apply_colormap(None, 4, 4, 16, None, 0, 0.0, 0.0, None, 12) == N.TSM_ERR_ARGUMENT
+    assert lib.tsm_reproject_to_depth_device(None, 4, 4, 16, 1.0, 1.0, None, 16, None) == N.TSM_ERR_ARGUMENT
+    assert lib.tsm_remap_linear_fixed_device(None, 4, 4, 12, 3, None, 16, None, 8, 4, 4, None, 12,
+                                             None) == N.TSM_ERR_ARGUMENT
+    assert lib.tsm_write_point_cloud_pcd(None, 0, None, 0, 0, 0, b"x.pcd") == N.TSM_ERR_ARGUMENT
 
 
 def test_version_and_device_count():

@@ -1,0 +1,207 @@
+"""SURVEY §8f f2-f4 on a real MI355X: the gfx950 kernels against the oracle
+(oracle/stereo_ops.c), host and device entry points, odd sizes and strides, the edge
+values the reference's loops meet (negative / inf / NaN disparities, borders).
+
+Bar: bit-exact, except reprojectTo3D(Q), whose reference product is cv::gemm with an
+unstated summation order: relative 1e-6 there (fp32, four terms).
+"""
+import ctypes
+import os
+
+import numpy as np
+import pytest
+
+from conftest import GOLDEN, load_bgr
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def tsm():
+    import tea_stereo_matching_amd as T
+
+    if T.device_count() == 0:
+        pytest.fail("no HIP device visible to a -m gpu test")
+    return T
+
+
+def _disp(rng, H, W, invalid=True):
+    d = rng.uniform(0, 192, (H, W)).astype(np.float32)
+    d[rng.random((H, W)) < 0.1] = np.float32(rng.choice([0.0, 1.0, 64.0, 191.0]))
+    if invalid:
+        m = rng.random((H, W))
+        d[m < 0.05] = -1.0
+        d[(m >= 0.05) & (m < 0.08)] = -2.0
+        d[(m >= 0.08) & (m < 0.09)] = np.inf
+        d[(m >= 0.09) & (m < 0.095)] = np.nan
+        d[(m >= 0.095) & (m < 0.1)] = -0.0
+    return d
+
+
+SIZES = [(1, 1), (3, 5), (37, 61), (375, 1242), (64, 1023)]
+
+
+@pytest.mark.parametrize("H,W", SIZES)
+def test_colormap_bit_exact(tsm, oracle, H, W):
+    rng = np.random.default_rng(H * 1000 + W)
+    d = _disp(rng, H, W)
+    lut = tsm.JETColorMap()
+    assert np.array_equal(tsm.applyColorMap(d, lut), oracle.apply_colormap_ex(d))
+    assert np.array_equal(tsm.applyColorMap(d, 10.0, 150.0, lut),
+                          oracle.apply_colormap_ex(d, min_val=10.0, max_val=150.0))
+    # a non-JET table goes through unchanged
+    gray = np.repeat(np.arange(256, dtype=np.uint8)[:, None], 3, 1)
+    assert np.array_equal(tsm.applyColorMap(d, gray), oracle.apply_colormap_ex(d, gray))
+
+
+def test_colormap_degenerate_ranges(tsm, oracle):
+    for d in (np.full((4, 9), 5.0, np.float32), np.full((4, 9), -1.0, np.float32),
+              np.array([[np.inf, -1.0, np.nan]], np.float32)):
+        assert np.array_equal(tsm.applyColorMap(d, tsm.JETColorMap()), oracle.apply_colormap_ex(d))
+
+
+def test_colormap_of_gpu_disparity_renders_reference_png(tsm):
+    """f2 end to end against the reference's own output: the GPU matcher (T = 20 race
+    emulation) + the GPU colour map reproduce demo-output/0600_adcensus.png exactly."""
+    d = os.path.join(GOLDEN, "demo")
+    left, right = load_bgr(os.path.join(d, "0600-Left.png")), load_bgr(os.path.join(d, "0600-Right.png"))
+    m = tsm.ADCensus(0)
+    try:
+        m.setMatchingStrategy(tsm.ColorModel.RGB, False, False)
+        m.setMinMaxDisparity(0, 192)
+        m.setOmpEmulation(20)
+        disp = m.compute(left, right)
+    finally:
+        m.close()
+    col = tsm.applyColorMap(disp, tsm.JETColorMap())
+    ref = load_bgr(os.path.join(d, "0600_adcensus.png"))
+    assert np.array_equal(col, ref), f"{(col != ref).any(-1).sum()} pixels differ"
+
+
+@pytest.mark.parametrize("H,W", SIZES)
+def test_reprojection_bit_exact(tsm, oracle, H, W):
+    rng = np.random.default_rng(7 * H + W)
+    d = _disp(rng, H, W)
+    f, b, cx, cy = 721.5377, 0.5327, 609.5593, 172.854
+    assert np.array_equal(tsm.reprojectToDepth(d, f, b), oracle.reproject_to_depth(d, f, b), equal_nan=True)
+    assert np.array_equal(tsm.reprojectTo3D(d, f, b, cx, cy), oracle.reproject_to_3d(d, f, b, cx, cy),
+                          equal_nan=True)
+
+
+def test_reprojection_q_within_tolerance(tsm, oracle):
+    rng = np.random.default_rng(9)
+    d = rng.uniform(1, 192, (375, 1242)).astype(np.float32)
+    f, b, cx, cy = 721.5377, 0.5327, 609.5593, 172.854
+    Q = np.array([[1, 0, 0, -cx], [0, 1, 0, -cy], [0, 0, 0, f], [0, 0, 1 / b, 0]], np.float64)
+    np.testing.assert_allclose(tsm.reprojectTo3D(d, Q), oracle.reproject_to_3d_q(d, Q), rtol=1e-6, atol=1e-6)
+
+
+class _Hip:
+    """Device buffers through the HIP runtime the library itself links (not torch's
+    bundled copy: two runtimes in one process do not share a device context)."""
+
+    def __init__(self):
+        self.rt = ctypes.CDLL("libamdhip64.so.7")
+        self.bufs = []
+
+    def put(self, a: np.ndarray) -> ctypes.c_void_p:
+        p = ctypes.c_void_p()
+        assert self.rt.hipMalloc(ctypes.byref(p), ctypes.c_size_t(max(a.nbytes, 1))) == 0
+        self.bufs.append(p)
+        assert self.rt.hipMemcpy(p, a.ctypes.data_as(ctypes.c_void_p), ctypes.c_size_t(a.nbytes), 1) == 0
+        return p
+
+    def get(self, p, like: np.ndarray) -> np.ndarray:
+        out = np.empty_like(like)
+        assert self.rt.hipDeviceSynchronize() == 0
+        assert self.rt.hipMemcpy(out.ctypes.data_as(ctypes.c_void_p), p, ctypes.c_size_t(out.nbytes), 2) == 0
+        return out
+
+    def free(self):
+        for p in self.bufs:
+            self.rt.hipFree(p)
+
+
+def test_device_forms_match_oracle(tsm, oracle):
+    from tea_stereo_matching_amd import _native as N
+
+    lib = N.load()
+    hip = _Hip()
+    try:
+        rng = np.random.default_rng(21)
+        H, W = 375, 1242
+        d = _disp(rng, H, W)
+        dd = hip.put(d)
+        lut = tsm.JETColorMap()
+        col = np.zeros((H, W, 3), np.uint8)
+        dc = hip.put(col)
+        for rep in range(3):  # repeated launches reuse the per-stream min/max scratch
+            assert lib.tsm_apply_colormap_device(dd, H, W, 4 * W, lut.ctypes.data_as(ctypes.c_void_p), 0,
+                                                 0.0, 0.0, dc, 3 * W, None) == 0
+            assert np.array_equal(hip.get(dc, col), oracle.apply_colormap_ex(d))
+        dep = np.zeros((H, W), np.float32)
+        dp = hip.put(dep)
+        assert lib.tsm_reproject_to_depth_device(dd, H, W, 4 * W, 700.0, 0.5, dp, 4 * W, None) == 0
+        assert np.array_equal(hip.get(dp, dep), oracle.reproject_to_depth(d, 700.0, 0.5), equal_nan=True)
+        xyz = np.zeros((H, W, 3), np.float32)
+        dx = hip.put(xyz)
+        assert lib.tsm_reproject_to_3d_device(dd, H, W, 4 * W, 700.0, 0.5, 620.0, 187.0, dx, 12 * W, None) == 0
+        assert np.array_equal(hip.get(dx, xyz), oracle.reproject_to_3d(d, 700.0, 0.5, 620.0, 187.0),
+                              equal_nan=True)
+    finally:
+        hip.free()
+
+
+def _maps(rng, H, W, sh, sw):
+    # a smooth warp (rotation + radial term) around the image, reaching past the borders
+    yy, xx = np.mgrid[0:H, 0:W].astype(np.float32)
+    cx, cy = sw / 2, sh / 2
+    a = np.float32(0.03)
+    r2 = ((xx - cx) ** 2 + (yy - cy) ** 2) / np.float32(max(sw, sh) ** 2)
+    k = np.float32(1) + np.float32(0.08) * r2
+    mx = (cx + k * (np.cos(a) * (xx - cx) - np.sin(a) * (yy - cy)) * np.float32(sw / W)).astype(np.float32)
+    my = (cy + k * (np.sin(a) * (xx - cx) + np.cos(a) * (yy - cy)) * np.float32(sh / H)).astype(np.float32)
+    mx += rng.uniform(-0.5, 0.5, mx.shape).astype(np.float32)
+    ix = np.rint(mx * np.float32(32)).astype(np.int64)
+    iy = np.rint(my * np.float32(32)).astype(np.int64)
+    xy = np.stack([ix >> 5, iy >> 5], -1).astype(np.int16)
+    fxy = ((iy & 31) * 32 + (ix & 31)).astype(np.uint16)
+    return mx, my, xy, fxy
+
+
+@pytest.mark.parametrize("C", [1, 3, 4])
+@pytest.mark.parametrize("H,W", [(1, 1), (17, 23), (375, 1242), (120, 161)])
+def test_remap_bit_exact(tsm, oracle, C, H, W):
+    rng = np.random.default_rng(C * 100 + H)
+    sh, sw = max(H + 3, 2), max(W - 5, 2)
+    src = rng.integers(0, 256, (sh, sw, C) if C > 1 else (sh, sw), dtype=np.uint8)
+    mx, my, xy, fxy = _maps(rng, H, W, sh, sw)
+    assert np.array_equal(tsm.remap(src, xy, fxy), oracle.remap_linear_fixed(src, xy, fxy))
+    assert np.array_equal(tsm.remap(src, mx, my), oracle.remap_linear_float(src, mx, my))
+
+
+def test_remap_float_map_edge_values(tsm, oracle):
+    rng = np.random.default_rng(4)
+    src = rng.integers(0, 256, (30, 40, 3), dtype=np.uint8)
+    mx = rng.uniform(-2, 42, (12, 16)).astype(np.float32)
+    my = rng.uniform(-2, 32, (12, 16)).astype(np.float32)
+    mx[0, :4] = [np.nan, np.inf, -np.inf, 1e12]
+    my[1, :4] = [np.nan, 3e9, -3e9, 0.015625]  # 1/64: a tie at 1/32 resolution (rounds to even)
+    mx[2, :3] = [0.015625, 0.046875, 39.99]
+    assert np.array_equal(tsm.remap(src, mx, my), oracle.remap_linear_float(src, mx, my))
+
+
+def test_epipolar_rectify_side_by_side(tsm, oracle):
+    rng = np.random.default_rng(8)
+    H, W = 96, 128
+    left = rng.integers(0, 256, (H, W, 3), dtype=np.uint8)
+    right = rng.integers(0, 256, (H, W, 3), dtype=np.uint8)
+    _, _, xy0, f0 = _maps(rng, H, W, H, W)
+    _, _, xy1, f1 = _maps(rng, H, W, H, W)
+    m = tsm.EpipolarRectifyMap(map00=xy0, map01=f0, map10=xy1, map11=f1)
+    r = tsm.EpipolarRectify(m, (W, H))
+    both = r.rectify(np.concatenate([left, right], 1))
+    l2, r2 = r.rectify(left, right)
+    exp_l, exp_r = oracle.remap_linear_fixed(left, xy0, f0), oracle.remap_linear_fixed(right, xy1, f1)
+    assert np.array_equal(l2, exp_l) and np.array_equal(r2, exp_r)
+    assert np.array_equal(both, np.concatenate([exp_l, exp_r], 1))
