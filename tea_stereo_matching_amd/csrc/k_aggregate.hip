@@ -1047,6 +1047,10 @@ __global__ __launch_bounds__(AS_THREADS) void k_agg_stream(AggStream S, DevParam
 constexpr int AX_THREADS = 16 * 64;
 constexpr int AX_MW = 2;  // meta words per pixel: packed descriptor (lo, hi, size), RN(1/size)
 constexpr int AX_D = 12;  // A-wave staging ring: steps in flight (AX_D * 8 px * Q * 16 B per CU)
+constexpr int AX_MIR = 3;  // mirror slots after each ring (a 4-read block spans 3 slots past its start)
+constexpr int AX_MC = 12;  // meta ring chunks (B reads chunk s - LAG + 1 before A overwrites its slot)
+static_assert(AX_D == AS_RC1 && AX_D == AS_RC2 && AX_D == AX_MC, "ring slots are compile-time per unrolled step");
+static_assert(AS_AHEAD + AS_LAG <= AX_MC, "meta ring too short for the B lag");
 
 template <bool FUSED, int QT>
 __global__ __launch_bounds__(AX_THREADS) void k_agg_split(AggStream S, DevParams Pk) {
@@ -1064,9 +1068,10 @@ __global__ __launch_bounds__(AX_THREADS) void k_agg_split(AggStream S, DevParams
     const int my_lines = (S.nl - g + G - 1) / G;
     const int nch = my_lines * S.cpl;
     const uint32_t r1_off = 0;                                            // LDS byte offsets
-    const uint32_t r2_off = (uint32_t)AS_RP1 * Qs;
-    const uint32_t meta_off = r2_off + (uint32_t)AS_RP2 * Qs;
-    const uint32_t zero_off = meta_off + (uint32_t)AS_MC * AS_SEG * AX_MW * 4;
+    // each ring is followed by AX_MIR mirror slots (copies of its first slots), so a block of
+    // 4 window reads starting at any slot never wraps
+    const uint32_t r2_off = (uint32_t)(AS_RP1 + AX_MIR) * Qs;
+    const uint32_t meta_off = r2_off + (uint32_t)(AS_RP2 + AX_MIR) * Qs;
     const uint32_t r1_end = r1_off + (uint32_t)AS_RP1 * Qs, r2_end = r2_off + (uint32_t)AS_RP2 * Qs;
     char* lds = reinterpret_cast<char*>(smem_f4);
 
@@ -1085,14 +1090,15 @@ __global__ __launch_bounds__(AX_THREADS) void k_agg_split(AggStream S, DevParams
         return (size_t)v * vstride + (size_t)line * ls;
     };
     auto barrier = [&]() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); };
-    // sequential window sum of `len` ring pixels from LDS byte offset `off` in the ring
-    // [rb, re): blocks of 4 at immediate offsets while they do not wrap, then blocks whose
-    // slots past the window read the zero vector (x + 0.0 == x for the non-negative sums)
+    // sequential window sum of `len` ring pixels from LDS byte offset `off` (a slot of the
+    // ring [rb, re)): whole blocks of 4 at immediate offsets (the mirror slots make every
+    // block contiguous), then the 1-3 remaining pixels under uniform branches -- the
+    // reference's order, no padding reads, little scalar bookkeeping
     auto window = [&](uint32_t off, int len, uint32_t rb, uint32_t re) -> f32x4 {
         f32x4 acc = f32x4{0.f, 0.f, 0.f, 0.f};
         const char* lp = lds + lane16;
-        int j = 0;
-        for (; j + 4 <= len && off + 4 * Qs <= re; j += 4) {
+        const uint32_t span = re - rb;
+        for (int nb = len >> 2; nb > 0; --nb) {
             const char* p = lp + off;
             const f32x4 x0 = *reinterpret_cast<const f32x4*>(p);
             const f32x4 x1 = *reinterpret_cast<const f32x4*>(p + Qs);
@@ -1103,23 +1109,21 @@ __global__ __launch_bounds__(AX_THREADS) void k_agg_split(AggStream S, DevParams
             acc += x2;
             acc += x3;
             off += 4 * Qs;
-            off = off == re ? rb : off;
+            off = off >= re ? off - span : off;
         }
-        for (; j < len; j += 4) {
-            f32x4 x[4];
-#pragma unroll
-            for (int u = 0; u < 4; ++u) {
-                const uint32_t o = j + u < len ? off : zero_off;
-                x[u] = *reinterpret_cast<const f32x4*>(lp + o);
-                off += Qs;
-                off = off == re ? rb : off;
-            }
-#pragma unroll
-            for (int u = 0; u < 4; ++u) acc += x[u];
+        const int r = len & 3;
+        if (r) {
+            const char* p = lp + off;
+            const f32x4 x0 = *reinterpret_cast<const f32x4*>(p);
+            const f32x4 x1 = *reinterpret_cast<const f32x4*>(p + Qs);
+            const f32x4 x2 = *reinterpret_cast<const f32x4*>(p + 2 * Qs);
+            acc += x0;
+            if (r > 1) acc += x1;
+            if (r > 2) acc += x2;
         }
         return acc;
     };
-    const uint32_t mstep = AS_SEG * AX_MW * 4, mwrap = AS_MC * mstep;
+    const uint32_t mstep = AS_SEG * AX_MW * 4;
     const char* mbase = lds + meta_off + (uint32_t)w * AX_MW * 4;  // this wave's pixel column
 #ifdef TSM_EXP_STAMPS
     unsigned long long ast[3] = {0, 0, 0};
@@ -1164,8 +1168,10 @@ __global__ __launch_bounds__(AX_THREADS) void k_agg_split(AggStream S, DevParams
         // pixel w of chunk c -> ring1; its raw descriptor (arms, window size, reciprocal)
         // -> the meta ring (every lane writes the same 16 B: no exec branch)
         auto land = [&](const f32x4& val, uint32_t ma, uint32_t my, int c) {
-            *reinterpret_cast<f32x4*>(lds + r1_off + (uint32_t)((c % AS_RC1) * AS_SEG + w) * Qs + voff) = val;
-            *reinterpret_cast<u32x2*>(lds + meta_off + (uint32_t)((c % AS_MC) * AS_SEG + w) * AX_MW * 4) = u32x2{ma, my};
+            const int slot = (c % AS_RC1) * AS_SEG + w;
+            *reinterpret_cast<f32x4*>(lds + r1_off + (uint32_t)slot * Qs + voff) = val;
+            if (slot < AX_MIR) *reinterpret_cast<f32x4*>(lds + r1_off + (uint32_t)(AS_RP1 + slot) * Qs + voff) = val;
+            *reinterpret_cast<u32x2*>(lds + meta_off + (uint32_t)((c % AX_MC) * AS_SEG + w) * AX_MW * 4) = u32x2{ma, my};
         };
         // prologue: chunks 0 .. AHEAD + AX_D - 1 in flight, chunks 0 .. AHEAD - 1 landed.
         // Slot of chunk c: (c - AHEAD) mod AX_D, so step s lands and refills slot s mod AX_D.
@@ -1183,12 +1189,10 @@ __global__ __launch_bounds__(AX_THREADS) void k_agg_split(AggStream S, DevParams
 #pragma unroll
         for (int c = 0; c < AS_AHEAD; ++c) land(pre[c], pma[c], pmy[c], c);
         int ca = 0, cc_a = 0;  // pass-A chunk s: position in its line (validity of pixel w)
-        uint32_t r2w = r2_off + (uint32_t)w * Qs;  // ring2 slot of chunk s
-        uint32_t ma_off = 0;
-        int rp1 = w;  // ring1 pixel of chunk s, pixel w
+        // AX_D == ring chunks: every ring slot below is a compile-time function of u
         u32x2 mA;
         barrier();
-        mA = *reinterpret_cast<const u32x2*>(mbase + ma_off);
+        mA = *reinterpret_cast<const u32x2*>(mbase);
         for (int b = 0; b < nblk; ++b) {
 #pragma unroll
             for (int u = 0; u < AX_D; ++u) {
@@ -1203,23 +1207,23 @@ __global__ __launch_bounds__(AX_THREADS) void k_agg_split(AggStream S, DevParams
                 const float a_y = __uint_as_float(__builtin_amdgcn_readfirstlane(mA.y));
                 const float a_b = (float)(int)(arm >> 16);
                 const int lo = (int)(arm & 0xffu), hi = (int)((arm >> 8) & 0xffu);
-                int st = rp1 - lo;
+                int st = u * AS_SEG + w - lo;  // ring1 slot of chunk s pixel w, minus the arm
                 st = st < 0 ? st + AS_RP1 : st;
                 const uint32_t a_off = r1_off + (uint32_t)st * Qs;
                 const int a_len = lo + hi + 1;
-                rp1 = rp1 + AS_SEG >= AS_RP1 ? rp1 + AS_SEG - AS_RP1 : rp1 + AS_SEG;
-                ma_off += mstep;
-                ma_off = ma_off >= mwrap ? ma_off - mwrap : ma_off;
-                mA = *reinterpret_cast<const u32x2*>(mbase + ma_off);  // chunk s + 1 (landed)
+                mA = *reinterpret_cast<const u32x2*>(mbase + ((u + 1) % AX_MC) * mstep);  // chunk s + 1 (landed)
+                const uint32_t r2w = r2_off + (uint32_t)(u * AS_SEG + w) * Qs;  // ring2 slot of chunk s
                 if (s < nch && cc_a * AS_SEG + w < S.n) {
                     f32x4 acc = window(a_off, a_len, r1_off, r1_end);
                     if (S.ws) acc = div_ws(acc, a_b, a_y);
-                    if (vl) *reinterpret_cast<f32x4*>(lds + r2w + lane16) = acc;
+                    if (vl) {
+                        *reinterpret_cast<f32x4*>(lds + r2w + lane16) = acc;
+                        if (u == 0 && w < AX_MIR)
+                            *reinterpret_cast<f32x4*>(lds + r2w + (uint32_t)AS_RP2 * Qs + lane16) = acc;
+                    }
                 }
                 if (++cc_a == S.cpl) cc_a = 0;
                 (void)ca;
-                r2w += AS_SEG * Qs;
-                r2w = r2w >= r2_end ? r2w - (uint32_t)AS_RP2 * Qs : r2w;
                 AST_T(t2);
                 AST_ADD(2, t2 - t1);
                 barrier();
@@ -1242,28 +1246,24 @@ __global__ __launch_bounds__(AX_THREADS) void k_agg_split(AggStream S, DevParams
         if (++o.cc == S.cpl) { o.cc = 0; ++o.lidx; if (o.lidx < my_lines) o.off = line_base(o.lidx) + (size_t)w * es; }
         else o.off += (size_t)AS_SEG * es;
     };
-    if (wave == AS_SEG && vl) *reinterpret_cast<f32x4*>(lds + zero_off + lane16) = f32x4{0.f, 0.f, 0.f, 0.f};
     Out ob;
     out_init(ob);
-    const int lag = FUSED ? AS_LAG : 1;
-    uint32_t mb_off = (uint32_t)((AS_MC - lag % AS_MC) % AS_MC) * mstep;  // meta of chunk s - lag
-    uint32_t r2r = r2_off + (uint32_t)(((AS_RC2 - 1) % AS_RC2) * AS_SEG + w) * Qs;  // single: chunk s - 1
+    constexpr int lag = FUSED ? AS_LAG : 1;
     barrier();
-    uint32_t mB = *reinterpret_cast<const uint32_t*>(mbase + mb_off);  // arms of chunk s - lag
-    int rp2 = (AS_RP2 - lag * AS_SEG % AS_RP2 + w) % AS_RP2;             // its ring2 pixel
+    uint32_t mB = *reinterpret_cast<const uint32_t*>(mbase + ((AX_D - lag) % AX_MC) * mstep);  // arms of chunk -lag
     for (int b = 0; b < nblk; ++b) {
+#pragma unroll
         for (int u = 0; u < AX_D; ++u) {
             const int s = b * AX_D + u;
+            const int ub = (u - lag + 2 * AX_D) % AX_D;  // ring / meta chunk slot of chunk s - lag
             const uint32_t arm = __builtin_amdgcn_readfirstlane(mB);
             const int lo = (int)(arm & 0xffu), hi = (int)((arm >> 8) & 0xffu);
-            int st = rp2 - lo;
+            int st = ub * AS_SEG + w - lo;
             st = st < 0 ? st + AS_RP2 : st;
             const uint32_t b_off = r2_off + (uint32_t)st * Qs;
             const int b_len = lo + hi + 1;
-            rp2 = rp2 + AS_SEG >= AS_RP2 ? rp2 + AS_SEG - AS_RP2 : rp2 + AS_SEG;
-            mb_off += mstep;
-            mb_off = mb_off >= mwrap ? mb_off - mwrap : mb_off;
-            mB = *reinterpret_cast<const uint32_t*>(mbase + mb_off);
+            mB = *reinterpret_cast<const uint32_t*>(mbase + ((ub + 1) % AX_MC) * mstep);
+            const uint32_t r2r = r2_off + (uint32_t)(ub * AS_SEG + w) * Qs;  // single: chunk s - 1
             const int sb = s - lag;
             AST_T(t1);
             if (sb >= 0 && sb < nch) {
@@ -1273,10 +1273,6 @@ __global__ __launch_bounds__(AX_THREADS) void k_agg_split(AggStream S, DevParams
                     if (vl) *reinterpret_cast<f32x4*>(S.vol + ob.off + 4 * lane) = acc;
                 }
                 out_step(ob);
-            }
-            if (!FUSED) {
-                r2r += AS_SEG * Qs;
-                r2r = r2r >= r2_end ? r2r - (uint32_t)AS_RP2 * Qs : r2r;
             }
             AST_T(t2);
             AST_ADD(2, t2 - t1);
@@ -1290,7 +1286,7 @@ __global__ __launch_bounds__(AX_THREADS) void k_agg_split(AggStream S, DevParams
 
 static size_t agg_split_lds(const DevParams& P) {
     const int Q = P.Lp / 4;
-    return ((size_t)AS_RP1 + AS_RP2 + 1) * Q * 16 + (size_t)AS_MC * AS_SEG * AX_MW * 4;
+    return ((size_t)AS_RP1 + AS_RP2 + 2 * AX_MIR) * Q * 16 + (size_t)AX_MC * AS_SEG * AX_MW * 4;
 }
 
 static size_t agg_stream_lds(const DevParams& P, bool fused) {
