@@ -745,6 +745,7 @@ __device__ unsigned long long g_as_stamps[1024 * 16 * 4];  // [block][wave][barr
 //   [2] y = RN(1/windowSize)                                   [3] windowSize as float
 //   [4] LDS byte offset of the pass-B window start in ring2   [5] window length
 constexpr int AS_MW = 8;  // meta words per pixel
+constexpr int AX_MIR = 3;  // mirror slots after each ring (a 4-read block spans 3 slots past its start)
 
 // QT > 0: the pixel vector has QT float4 (compile-time ring stride); 0: runtime Q.
 template <bool FUSED, int QT>
@@ -764,9 +765,8 @@ __global__ __launch_bounds__(AS_THREADS) void k_agg_stream(AggStream S, DevParam
     const int my_lines = (S.nl - g + G - 1) / G;
     const int nch = my_lines * S.cpl;
     const uint32_t r1_off = 0;                                            // LDS byte offsets
-    const uint32_t r2_off = (uint32_t)AS_RP1 * Qs;
-    const uint32_t meta_off = r2_off + (FUSED ? (uint32_t)AS_RP2 * Qs : 0u);
-    const uint32_t zero_off = meta_off + (uint32_t)AS_MC * AS_SEG * AS_MW * 4;
+    const uint32_t r2_off = (uint32_t)(AS_RP1 + AX_MIR) * Qs;  // each ring + AX_MIR mirror slots
+    const uint32_t meta_off = r2_off + (FUSED ? (uint32_t)(AS_RP2 + AX_MIR) * Qs : 0u);
     char* lds = reinterpret_cast<char*>(smem_f4);
 
     const int tid = threadIdx.x;
@@ -859,6 +859,11 @@ __global__ __launch_bounds__(AS_THREADS) void k_agg_stream(AggStream S, DevParam
                 char* slot = lds + r1_off + (uint32_t)(c % AS_RC1) * AS_SEG * Qs + (uint32_t)lanec * 16;
 #pragma unroll
                 for (int i = 0; i < AS_SEG; ++i) *reinterpret_cast<f32x4*>(slot + i * Qs) = b[h * AS_SEG + i];
+                if (c % AS_RC1 == 0) {  // ring slots 0..AX_MIR-1 are mirrored past the ring's end
+#pragma unroll
+                    for (int i = 0; i < AX_MIR; ++i)
+                        *reinterpret_cast<f32x4*>(slot + (AS_RP1 + i) * Qs) = b[h * AS_SEG + i];
+                }
             }
             if (lane < NG * AS_SEG) {  // window descriptors of the turn's pixels
                 const int hh = lane >> 3, c = NG * k + hh, px = lane & 7;
@@ -916,17 +921,16 @@ __global__ __launch_bounds__(AS_THREADS) void k_agg_stream(AggStream S, DevParam
 
     // ---- summing waves -------------------------------------------------------------
     // Sequential window sum of `len` ring pixels from LDS byte offset `off` in the ring
-    // [rb, re).  Whole blocks of 4 that do not wrap read at immediate offsets; the last
-    // (partial) block and wrapping blocks go pixel by pixel, slots past the window
-    // reading the zero vector (a scalar select): x + 0.0 == x for the non-negative sums.
+    // [rb, re): whole blocks of 4 at immediate offsets (AX_MIR mirror slots past each ring
+    // make every block contiguous), then the 1-3 remaining pixels under uniform branches.
     auto window = [&](uint32_t off, int len, uint32_t rb, uint32_t re) -> f32x4 {
         f32x4 acc = f32x4{0.f, 0.f, 0.f, 0.f};
         const char* lp = lds + lane16;
 #ifdef TSM_EXP_AGG_W1
         return *reinterpret_cast<const f32x4*>(lp + off);  // timing experiment only
 #endif
-        int j = 0;
-        for (; j + 4 <= len && off + 4 * Qs <= re; j += 4) {
+        const uint32_t span = re - rb;
+        for (int nb = len >> 2; nb > 0; --nb) {
             const char* p = lp + off;
             const f32x4 x0 = *reinterpret_cast<const f32x4*>(p);
             const f32x4 x1 = *reinterpret_cast<const f32x4*>(p + Qs);
@@ -937,19 +941,17 @@ __global__ __launch_bounds__(AS_THREADS) void k_agg_stream(AggStream S, DevParam
             acc += x2;
             acc += x3;
             off += 4 * Qs;
-            off = off == re ? rb : off;
+            off = off >= re ? off - span : off;
         }
-        for (; j < len; j += 4) {
-            f32x4 x[4];
-#pragma unroll
-            for (int u = 0; u < 4; ++u) {
-                const uint32_t o = j + u < len ? off : zero_off;
-                x[u] = *reinterpret_cast<const f32x4*>(lp + o);
-                off += Qs;
-                off = off == re ? rb : off;
-            }
-#pragma unroll
-            for (int u = 0; u < 4; ++u) acc += x[u];
+        const int r = len & 3;
+        if (r) {
+            const char* p = lp + off;
+            const f32x4 x0 = *reinterpret_cast<const f32x4*>(p);
+            const f32x4 x1 = *reinterpret_cast<const f32x4*>(p + Qs);
+            const f32x4 x2 = *reinterpret_cast<const f32x4*>(p + 2 * Qs);
+            acc += x0;
+            if (r > 1) acc += x1;
+            if (r > 2) acc += x2;
         }
         return acc;
     };
@@ -968,7 +970,6 @@ __global__ __launch_bounds__(AS_THREADS) void k_agg_stream(AggStream S, DevParam
         if (++o.cc == S.cpl) { o.cc = 0; ++o.lidx; if (o.lidx < my_lines) o.off = line_base(o.lidx) + (size_t)wave * es; }
         else o.off += (size_t)AS_SEG * es;
     };
-    if (wave == 0 && vl) *reinterpret_cast<f32x4*>(lds + zero_off + lane16) = f32x4{0.f, 0.f, 0.f, 0.f};
     asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");  // prologue chunks landed
     Out oa, ob;
     out_init(oa);
@@ -1012,7 +1013,11 @@ __global__ __launch_bounds__(AS_THREADS) void k_agg_stream(AggStream S, DevParam
                 f32x4 acc = window(a_off, a_len, r1_off, r1_end);
                 if (S.ws) acc = div_ws(acc, a_b, a_y);
                 if (FUSED) {
-                    if (vl) *reinterpret_cast<f32x4*>(lds + r2w + lane16) = acc;
+                    if (vl) {
+                        *reinterpret_cast<f32x4*>(lds + r2w + lane16) = acc;
+                        if (r2w < r2_off + (uint32_t)AX_MIR * Qs)
+                            *reinterpret_cast<f32x4*>(lds + r2w + (uint32_t)AS_RP2 * Qs + lane16) = acc;
+                    }
                 } else if (vl && (st_ok || acc.x == -1.f)) {
                     *reinterpret_cast<f32x4*>(S.vol + oa.off + 4 * lane) = acc;
                 }
@@ -1047,7 +1052,6 @@ __global__ __launch_bounds__(AS_THREADS) void k_agg_stream(AggStream S, DevParam
 constexpr int AX_THREADS = 16 * 64;
 constexpr int AX_MW = 2;  // meta words per pixel: packed descriptor (lo, hi, size), RN(1/size)
 constexpr int AX_D = 12;  // A-wave staging ring: steps in flight (AX_D * 8 px * Q * 16 B per CU)
-constexpr int AX_MIR = 3;  // mirror slots after each ring (a 4-read block spans 3 slots past its start)
 constexpr int AX_MC = 12;  // meta ring chunks (B reads chunk s - LAG + 1 before A overwrites its slot)
 static_assert(AX_D == AS_RC1 && AX_D == AS_RC2 && AX_D == AX_MC, "ring slots are compile-time per unrolled step");
 static_assert(AS_AHEAD + AS_LAG <= AX_MC, "meta ring too short for the B lag");
@@ -1291,7 +1295,7 @@ static size_t agg_split_lds(const DevParams& P) {
 
 static size_t agg_stream_lds(const DevParams& P, bool fused) {
     const int Q = P.Lp / 4;
-    return ((size_t)AS_RP1 + (fused ? AS_RP2 : 0) + 1) * Q * 16 + (size_t)AS_MC * AS_SEG * AS_MW * 4;
+    return ((size_t)AS_RP1 + AX_MIR + (fused ? AS_RP2 + AX_MIR : 0)) * Q * 16 + (size_t)AS_MC * AS_SEG * AS_MW * 4;
 }
 
 template <bool FUSED>
