@@ -14,7 +14,8 @@ disparity maps over RCCL.  Weak scaling: per-GPU work is fixed as N grows.
 Rank 0 prints ONE JSON line.  `roofline` prices the kernel named by BASELINE.json (the
 cost-volume build) from HIP events around its launches on the pipeline's stream, in an
 untimed phase after the timed region where one pipeline runs alone (in the timed region
-two pipelines overlap, so a kernel's event span would include its neighbours' work);
+`--concurrency` pipelines overlap, so a kernel's event span would include its
+neighbours' work); `next_rows` times the f2-f4 operators on the pipeline's outputs;
 `cpu_baseline` times the oracle (the C restatement of the reference's OpenMP path)
 on one pair on this host's cores.
 """
@@ -36,10 +37,10 @@ HBM_PEAK_GBS = 8000.0  # MI355X HBM3E peak (MI355X_MICROARCH.md chip table)
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--batch", type=int, default=8, help="pairs per GPU per step")
-    ap.add_argument("--concurrency", type=int, default=2, help="pair pipelines in flight per GPU")
+    ap.add_argument("--concurrency", type=int, default=4, help="pair pipelines in flight per GPU")
     ap.add_argument("--height", type=int, default=375)
     ap.add_argument("--width", type=int, default=1242)
     ap.add_argument("--max-disparity", type=int, default=192)
