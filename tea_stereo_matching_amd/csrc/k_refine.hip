@@ -313,6 +313,66 @@ __global__ void k_interp(const int32_t* __restrict__ disp, int32_t* __restrict__
     out[idx] = res;
 }
 
+// Ray-parallel form: 16 lanes per pixel, lane = ray, 4 pixels of a row per wave.  The
+// rays' dependent load chains (<= max_search_depth steps each) run side by side instead
+// of one after another; the per-ray results are then folded in ray order exactly as
+// above (a min for occlusions, the colour-difference rule for mismatches).
+__global__ __launch_bounds__(256) void k_interp_rays(const int32_t* __restrict__ disp, int32_t* __restrict__ out,
+                                                     const uint32_t* __restrict__ img0, DevParams Pk) {
+    const DevParams P = Pk;
+    const int lane = threadIdx.x & 63;
+    const int dir = lane & 15;
+    const int x = (blockIdx.x * blockDim.x + threadIdx.x) >> 4;  // 16 lanes per pixel
+    const int y = blockIdx.y;
+    const int H = P.H, W = P.W, minD = P.minD;
+    const bool inside = x < W;
+    const size_t idx = (size_t)y * W + (inside ? x : W - 1);
+    const int cur = disp[idx];
+    const bool outlier = inside && cur < minD;
+    if (!__any(outlier)) {  // the whole wave: no outlier
+        if (inside && dir == 0) out[idx] = cur;
+        return;
+    }
+    int nd = cur, ndiff = -1;
+    if (outlier) {
+        const uint32_t c0 = img0[idx];
+        const int rh = c_ray_h[dir], rw = c_ray_w[dir];
+        const int sh0 = rh / 2, sh1 = rh - rh / 2, sw0 = rw / 2, sw1 = rw - rw / 2;
+        int hD = y, wD = x;
+        for (int s = 0; s < P.max_search_depth; ++s) {
+            hD += (s & 1) ? sh1 : sh0;
+            wD += (s & 1) ? sw1 : sw0;
+            if (hD < 0 || hD >= H || wD < 0 || wD >= W) break;
+            const int dv = disp[(size_t)hD * W + wD];
+            if (dv >= minD) {
+                nd = dv;
+                ndiff = color_diff(P, c0, img0[(size_t)hD * W + wD]);
+                break;
+            }
+        }
+    }
+    // fold the 16 rays of this lane's pixel in ray order (every lane of the group
+    // computes the same result; lane dir == 0 writes it)
+    const int base = lane & ~15;
+    const bool occlusion = cur == minD - 1;  // :1209
+    int res = 0, mdiff = -1;
+#pragma unroll
+    for (int d = 0; d < 16; ++d) {
+        const int n_d = __shfl(nd, base + d);
+        const int f_d = __shfl(ndiff, base + d);
+        if (occlusion) {
+            res = d == 0 ? n_d : min(res, n_d);
+        } else if (d == 0) {
+            res = n_d;
+            mdiff = f_d;
+        } else if (mdiff < 0 || (mdiff > f_d && f_d > 0)) {
+            res = n_d;
+            mdiff = f_d;
+        }
+    }
+    if (inside && dir == 0) out[idx] = outlier ? res : cur;
+}
+
 // ---------------------------------------------------------------------------
 // discontinuity adjustment: gray -> equalizeHist -> blur -> Canny -> adjust
 // ---------------------------------------------------------------------------
@@ -646,7 +706,15 @@ void launch_region_voting(RefineBufs& B, const uint32_t* arms0, int hf, const De
 
 void launch_interpolation(RefineBufs& B, const uint32_t* img0, const DevParams& P,
                           hipStream_t st) {
-    hipLaunchKernelGGL(k_interp, grid2d(P.W, P.H, 128), dim3(128), 0, st, B.dm, B.dtmp, img0, P); trace_point("k_interp", st);
+    static const bool serial = [] {
+        const char* e = getenv("TSM_INTERP_SERIAL");  // A/B: the one-thread-per-pixel form
+        return e && e[0] == '1';
+    }();
+    if (serial)
+        hipLaunchKernelGGL(k_interp, grid2d(P.W, P.H, 128), dim3(128), 0, st, B.dm, B.dtmp, img0, P);
+    else
+        hipLaunchKernelGGL(k_interp_rays, grid2d(P.W * 16, P.H, 256), dim3(256), 0, st, B.dm, B.dtmp, img0, P);
+    trace_point("k_interp", st);
     std::swap(B.dm, B.dtmp);
 }
 
