@@ -98,6 +98,68 @@ __global__ void k_vote_count(const int32_t* __restrict__ disp, int32_t* __restri
     flags[idx] = 1 | (cnt > P.voting_thresh ? 2 : 0);
 }
 
+// The same with 16 lanes per pixel (4 pixels of a row per wave): lanes take every 16th
+// outer-arm position, the counts are summed over the group, and only a low-vote outlier
+// (every valid sample kept) walks its region a second time to write the samples at the
+// lanes' prefix positions.  A sample's slot does not matter (k_vote_decide histograms
+// them), only that all of them are kept.
+__global__ __launch_bounds__(256) void k_vote_count_par(const int32_t* __restrict__ disp,
+                                                        int32_t* __restrict__ dtmp,
+                                                        const uint32_t* __restrict__ arms,
+                                                        int32_t* __restrict__ vote,
+                                                        uint16_t* __restrict__ samples,
+                                                        uint8_t* __restrict__ flags, int hf, DevParams Pk) {
+    const DevParams P = Pk;
+    const int lane = threadIdx.x & 63, sub = lane & 15, base = lane & ~15;
+    const int x = (blockIdx.x * blockDim.x + threadIdx.x) >> 4;
+    const int y = blockIdx.y;
+    const int W = P.W, minD = P.minD;
+    const bool inside = x < W;
+    const size_t idx = (size_t)y * W + (inside ? x : W - 1);
+    const int cur = disp[idx];
+    const bool outlier = inside && cur < minD;
+    if (inside && sub == 0) dtmp[idx] = cur;  // dispTemp starts as the input
+    if (!__any(outlier)) {
+        if (inside && sub == 0) { flags[idx] = 0; vote[idx] = 0; }
+        return;
+    }
+    int oA = 0, oB = -1, iA, iB;
+    if (outlier) region_arms(arms[idx], hf, oA, oB, iA, iB);
+    // walk the outer positions o = -oA + sub + 16 k; `emit` writes the valid samples
+    auto walk = [&](bool emit, int pos, uint16_t* smp) {
+        int cnt = 0;
+        for (int o = -oA + sub; o <= oB; o += 16) {
+            const int yy0 = hf ? y + o : y, xx0 = hf ? x : x + o;
+            int a1, b1, a2, b2;
+            region_arms(arms[(size_t)yy0 * W + xx0], hf, a1, b1, a2, b2);
+            const ptrdiff_t st = hf ? 1 : W;
+            const int32_t* rp = disp + (size_t)yy0 * W + xx0;
+            for (int i = -a2; i <= b2; ++i) {
+                const int dv = rp[(ptrdiff_t)i * st];
+                if (dv >= minD) {
+                    if (emit) smp[pos + cnt] = (uint16_t)(dv - minD);
+                    cnt++;
+                }
+            }
+        }
+        return cnt;
+    };
+    const int mine = outlier ? walk(false, 0, nullptr) : 0;
+    // inclusive prefix over the 16 lanes of the group
+    int incl = mine;
+#pragma unroll
+    for (int d = 1; d < 16; d <<= 1) {
+        const int v = __shfl_up(incl, d, 16);
+        if (sub >= d) incl += v;
+    }
+    const int total = __shfl(incl, base + 15);
+    if (outlier && total <= kMaxSamples && mine > 0) walk(true, incl - mine, samples + idx * kMaxSamples);
+    if (inside && sub == 0) {
+        vote[idx] = outlier ? total : 0;
+        flags[idx] = outlier ? (uint8_t)(1 | (total > P.voting_thresh ? 2 : 0)) : 0;
+    }
+}
+
 // Device-wide exclusive scan of the two flag counters in raster order:
 //   out_pos[p]  = # outliers before p        out_list[out_pos[p]] = p
 //   hi_list[r]  = r-th high-vote outlier      counts = {#outliers, #high-vote}
@@ -692,8 +754,17 @@ void launch_region_voting(RefineBufs& B, const uint32_t* arms0, int hf, const De
                           hipStream_t st) {
     const int n = P.H * P.W;
     const int nb = (int)refine_scan_blocks(n);
-    hipLaunchKernelGGL(k_vote_count, grid2d(P.W, P.H, 128), dim3(128), 0, st, B.dm, B.dtmp, arms0,
-                       B.vote, B.samples, B.flags, hf, P); trace_point("k_vote_count", st);
+    static const bool serial = [] {
+        const char* e = getenv("TSM_VOTE_SERIAL");  // A/B: the one-thread-per-pixel count
+        return e && e[0] == '1';
+    }();
+    if (serial)
+        hipLaunchKernelGGL(k_vote_count, grid2d(P.W, P.H, 128), dim3(128), 0, st, B.dm, B.dtmp, arms0,
+                           B.vote, B.samples, B.flags, hf, P);
+    else
+        hipLaunchKernelGGL(k_vote_count_par, grid2d(P.W * 16, P.H, 256), dim3(256), 0, st, B.dm, B.dtmp,
+                           arms0, B.vote, B.samples, B.flags, hf, P);
+    trace_point("k_vote_count", st);
     hipLaunchKernelGGL(k_scan_count, dim3(nb), dim3(SC_THREADS), 0, st, B.flags, n, B.bsum); trace_point("k_scan_count", st);
     hipLaunchKernelGGL(k_scan_blocks, dim3(1), dim3(SC_THREADS), 0, st, B.bsum, nb, B.counts); trace_point("k_scan_blocks", st);
     hipLaunchKernelGGL(k_scan_scatter, dim3(nb), dim3(SC_THREADS), 0, st, B.flags, n, B.bsum,
