@@ -601,6 +601,79 @@ __global__ void k_uf_merge(const uint8_t* __restrict__ map, int32_t* __restrict_
     }
 }
 
+// Tiled form: union-find inside a 32x32 tile in LDS (LDS atomics), global labels are
+// the tile roots' pixel indices; then only the pairs crossing a tile edge merge in global
+// memory.  Same components as k_uf_merge.
+constexpr int UT = 32;
+
+__device__ __forceinline__ int lds_find(int* lab, int x) {
+    int p = __hip_atomic_load(&lab[x], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    while (p != x) {
+        x = p;
+        p = __hip_atomic_load(&lab[x], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    }
+    return x;
+}
+__device__ __forceinline__ void lds_union(int* lab, int a, int b) {
+    while (true) {
+        a = lds_find(lab, a);
+        b = lds_find(lab, b);
+        if (a == b) return;
+        if (a < b) { const int t = a; a = b; b = t; }
+        const int old = atomicCAS(&lab[a], a, b);
+        if (old == a) return;
+        a = old;
+    }
+}
+
+__global__ __launch_bounds__(256) void k_uf_tile(const uint8_t* __restrict__ map, int32_t* __restrict__ label,
+                                                 int H, int W) {
+    __shared__ int lab[UT * UT];
+    const int tx0 = blockIdx.x * UT, ty0 = blockIdx.y * UT;
+    for (int k = threadIdx.x; k < UT * UT; k += 256) {
+        const int x = tx0 + (k % UT), y = ty0 + k / UT;
+        lab[k] = (x < W && y < H && map[(size_t)y * W + x] != 1) ? k : -1;
+    }
+    __syncthreads();
+    for (int k = threadIdx.x; k < UT * UT; k += 256) {
+        if (lab[k] < 0) continue;
+        const int lx = k % UT, ly = k / UT;
+        if (lx > 0 && lab[k - 1] >= 0) lds_union(lab, k, k - 1);
+        if (ly > 0) {
+            if (lx > 0 && lab[k - UT - 1] >= 0) lds_union(lab, k, k - UT - 1);
+            if (lab[k - UT] >= 0) lds_union(lab, k, k - UT);
+            if (lx + 1 < UT && lab[k - UT + 1] >= 0) lds_union(lab, k, k - UT + 1);
+        }
+    }
+    __syncthreads();
+    for (int k = threadIdx.x; k < UT * UT; k += 256) {
+        const int x = tx0 + (k % UT), y = ty0 + k / UT;
+        if (x >= W || y >= H) continue;
+        int g = -1;
+        if (lab[k] >= 0) {
+            const int r = lds_find(lab, k);
+            g = (ty0 + r / UT) * W + tx0 + r % UT;
+        }
+        label[(size_t)y * W + x] = g;
+    }
+}
+
+__global__ void k_uf_edges(const uint8_t* __restrict__ map, int32_t* __restrict__ label, int H, int W) {
+    const int x = blockIdx.x * blockDim.x + threadIdx.x;
+    const int y = blockIdx.y;
+    if (x >= W) return;
+    const int lx = x % UT, ly = y % UT;
+    if (ly != 0 && lx != 0 && lx != UT - 1) return;  // no neighbour pair leaves the tile
+    const int i = y * W + x;
+    if (map[i] == 1) return;
+    if (lx == 0 && x > 0 && map[i - 1] != 1) uf_union(label, i, i - 1);
+    if (y > 0) {
+        if ((lx == 0 || ly == 0) && x > 0 && map[i - W - 1] != 1) uf_union(label, i, i - W - 1);
+        if (ly == 0 && map[i - W] != 1) uf_union(label, i, i - W);
+        if ((ly == 0 || lx == UT - 1) && x + 1 < W && map[i - W + 1] != 1) uf_union(label, i, i - W + 1);
+    }
+}
+
 __global__ void k_uf_flatten_mark(const uint8_t* __restrict__ map, int32_t* __restrict__ label,
                                   uint8_t* __restrict__ strong, int n) {
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
@@ -801,8 +874,18 @@ void launch_discontinuity(RefineBufs& B, const float* vol0, const DevParams& P,
     hipLaunchKernelGGL(k_sobel, grid2d(P.W, P.H, 256), dim3(256), 0, st, B.blurred, B.dx, B.dy, B.mag, P.H, P.W); trace_point("k_sobel", st);
     hipLaunchKernelGGL(k_nms, grid2d(P.W, P.H, 256), dim3(256), 0, st, B.dx, B.dy, B.mag, B.map,
                        P.H, P.W, P.canny_low, P.canny_high); trace_point("k_nms", st);
-    hipLaunchKernelGGL(k_uf_init, dim3((n + 255) / 256), dim3(256), 0, st, B.map, B.label, n); trace_point("k_uf_init", st);
-    hipLaunchKernelGGL(k_uf_merge, grid2d(P.W, P.H, 256), dim3(256), 0, st, B.map, B.label, P.H, P.W); trace_point("k_uf_merge", st);
+    static const bool flat_uf = [] {
+        const char* e = getenv("TSM_UF_FLAT");  // A/B: global-memory union-find over every pair
+        return e && e[0] == '1';
+    }();
+    if (flat_uf) {
+        hipLaunchKernelGGL(k_uf_init, dim3((n + 255) / 256), dim3(256), 0, st, B.map, B.label, n); trace_point("k_uf_init", st);
+        hipLaunchKernelGGL(k_uf_merge, grid2d(P.W, P.H, 256), dim3(256), 0, st, B.map, B.label, P.H, P.W); trace_point("k_uf_merge", st);
+    } else {
+        hipLaunchKernelGGL(k_uf_tile, dim3((P.W + UT - 1) / UT, (P.H + UT - 1) / UT), dim3(256), 0, st, B.map,
+                           B.label, P.H, P.W); trace_point("k_uf_tile", st);
+        hipLaunchKernelGGL(k_uf_edges, grid2d(P.W, P.H, 256), dim3(256), 0, st, B.map, B.label, P.H, P.W); trace_point("k_uf_edges", st);
+    }
     hipLaunchKernelGGL(k_zero_u32, dim3((n / 4 + 256) / 256), dim3(256), 0, st, reinterpret_cast<uint32_t*>(B.strong), (n + 3) / 4); trace_point("k_zero_u32", st);
     hipLaunchKernelGGL(k_uf_flatten_mark, dim3((n + 255) / 256), dim3(256), 0, st, B.map, B.label, B.strong, n); trace_point("k_uf_flatten_mark", st);
     hipLaunchKernelGGL(k_uf_final, dim3((n + 255) / 256), dim3(256), 0, st, B.map, B.label, B.strong, B.edges, n); trace_point("k_uf_final", st);
