@@ -52,6 +52,30 @@ __global__ void k_outlier(const int32_t* __restrict__ dl, const int32_t* __restr
     out[(size_t)y * W + x] = d;
 }
 
+// Row form: the reference's occlusion search (does some k in [minD, maxD] have
+// dR(x - k) == k?) asks whether any right-view pixel c maps onto x (c + dR(c) == x), so
+// each row scatters that map into an LDS bitmap once and every pixel tests one byte.
+__global__ __launch_bounds__(256) void k_outlier_row(const int32_t* __restrict__ dl, const int32_t* __restrict__ dr,
+                                                     int32_t* __restrict__ out, DevParams Pk) {
+    const DevParams P = Pk;
+    extern __shared__ uint8_t hit[];
+    const int y = blockIdx.x;
+    const int W = P.W;
+    const int32_t* r = dr + (size_t)y * W;
+    for (int x = threadIdx.x; x < W; x += blockDim.x) hit[x] = 0;
+    __syncthreads();
+    for (int c = threadIdx.x; c < W; c += blockDim.x) {
+        const int k = r[c];
+        if (k >= P.minD && k <= P.maxD && c + k < W) hit[c + k] = 1;
+    }
+    __syncthreads();
+    for (int x = threadIdx.x; x < W; x += blockDim.x) {
+        int d = dl[(size_t)y * W + x];
+        if (x - d < 0 || iabs_(d - r[x - d]) > P.disp_tolerance) d = hit[x] ? -2 : -1;  // (:415-416)
+        out[(size_t)y * W + x] = d;
+    }
+}
+
 // ---------------------------------------------------------------------------
 // region voting
 // ---------------------------------------------------------------------------
@@ -819,7 +843,15 @@ size_t refine_scan_blocks(int n) { return (size_t)(n + SC_BLOCK - 1) / SC_BLOCK;
 static dim3 grid2d(int W, int H, int bx) { return dim3((W + bx - 1) / bx, H); }
 
 void launch_outlier(RefineBufs& B, const DevParams& P, hipStream_t st) {
-    hipLaunchKernelGGL(k_outlier, grid2d(P.W, P.H, 256), dim3(256), 0, st, B.disp0, B.disp1, B.dm, P); trace_point("k_outlier", st);
+    static const bool serial = [] {
+        const char* e = getenv("TSM_OUTLIER_SERIAL");  // A/B: the per-pixel disparity search
+        return e && e[0] == '1';
+    }();
+    if (serial)
+        hipLaunchKernelGGL(k_outlier, grid2d(P.W, P.H, 256), dim3(256), 0, st, B.disp0, B.disp1, B.dm, P);
+    else
+        hipLaunchKernelGGL(k_outlier_row, dim3(P.H), dim3(256), (size_t)P.W, st, B.disp0, B.disp1, B.dm, P);
+    trace_point("k_outlier", st);
 }
 
 // Each Jacobi stage reads B.dm, writes B.dtmp, then the two maps swap roles (no copies).
