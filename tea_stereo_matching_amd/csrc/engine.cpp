@@ -181,6 +181,7 @@ size_t workspace_bytes(int H, int W, int L) {
     b += 12 * N * 4;           // ws, reciprocals, packed descriptors
     b += 4 * (size_t)H * (W + 2 * grad_pad(L) + 16);  // gv, gh (upper bound)
     b += N * (4 * 8 + 2 * 20 + 1 * 6 + 2 * 2 + 4); // refine maps
+    b += N * (4 + 2 * 20);     // carried votes / samples by outlier rank
     return b;
 }
 
@@ -302,6 +303,8 @@ int ensure_workspace(tsm_adc* h, Workspace* w, int H, int W) {
     A(B.out_pos, N * 4);
     A(B.out_list, N * 4);
     A(B.hi_list, N * 4);
+    A(B.cvote, N * 4);
+    A(B.csamp, N * 20 * 2);
     A(B.bsum, 2 * refine_scan_blocks((int)N) * 4 + 64);
     A(B.counts, 16);
     A(B.gray, N);

@@ -266,6 +266,24 @@ __global__ void k_scan_scatter(const uint8_t* __restrict__ flags, int n,
     }
 }
 
+// The outliers' votes and low-vote samples laid out by outlier rank, so a high-vote
+// outlier's carry range is one contiguous run for k_vote_decide (thread per rank, the
+// 40-B sample record moved as ten dwords).
+__global__ void k_rank_samples(const int32_t* __restrict__ out_list, const int32_t* __restrict__ counts,
+                               const int32_t* __restrict__ vote, const uint16_t* __restrict__ samples,
+                               int32_t* __restrict__ cvote, uint16_t* __restrict__ csamp) {
+    const int a = blockIdx.x * blockDim.x + threadIdx.x;
+    if (a >= counts[0]) return;
+    const int p = out_list[a];
+    const int c = vote[p];
+    cvote[a] = c;
+    if (c > kMaxSamples) return;  // high-vote: never carried
+    const uint32_t* src = reinterpret_cast<const uint32_t*>(samples + (size_t)p * kMaxSamples);
+    uint32_t* dst = reinterpret_cast<uint32_t*>(csamp + (size_t)a * kMaxSamples);
+#pragma unroll
+    for (int i = 0; i < kMaxSamples / 2; ++i) dst[i] = src[i];
+}
+
 // One wave per high-vote outlier: LDS histogram of its own region + carried samples,
 // then the first argmax and the ratio test (:1137-1153).
 constexpr int VD_THREADS = 256;
@@ -273,7 +291,8 @@ constexpr int VD_THREADS = 256;
 __global__ __launch_bounds__(VD_THREADS) void k_vote_decide(
     const int32_t* __restrict__ disp, int32_t* __restrict__ dtmp, const uint32_t* __restrict__ arms,
     const int32_t* __restrict__ vote, const uint16_t* __restrict__ samples,
-    const int32_t* __restrict__ out_pos, const int32_t* __restrict__ out_list,
+    const int32_t* __restrict__ out_pos, const int32_t* __restrict__ cvote,
+    const uint16_t* __restrict__ csamp,
     const int32_t* __restrict__ hi_list, const int32_t* __restrict__ counts, int hf, DevParams Pk) {
     const DevParams P = Pk;  // kernel args -> registers once (no per-use kernarg reloads)
     extern __shared__ int hist_all[];
@@ -314,19 +333,17 @@ __global__ __launch_bounds__(VD_THREADS) void k_vote_decide(
         // carried low-vote outliers: (previous high-vote outlier, p) in raster order
         const int k0 = r > 0 ? out_pos[hi_list[r - 1]] + 1 : 0;
         const int k1 = out_pos[p];
+        // (rank-ordered copies: consecutive lanes read consecutive 40-B sample records,
+        // one load round trip per entry)
         for (int k = k0 + lane; k < k1; k += 64) {
-            const int qp = out_list[k];
-            const int c = vote[qp];
-            const uint16_t* s = samples + (size_t)qp * kMaxSamples;
-            int m = 0;
-            for (; m + 3 < c; m += 4) {
-                const int s0 = s[m], s1 = s[m + 1], s2 = s[m + 2], s3 = s[m + 3];
-                atomicAdd(&hist[s0], 1);
-                atomicAdd(&hist[s1], 1);
-                atomicAdd(&hist[s2], 1);
-                atomicAdd(&hist[s3], 1);
-            }
-            for (; m < c; ++m) atomicAdd(&hist[s[m]], 1);
+            const int c = cvote[k];
+            const uint32_t* s = reinterpret_cast<const uint32_t*>(csamp + (size_t)k * kMaxSamples);
+            uint32_t wv[kMaxSamples / 2];
+#pragma unroll
+            for (int i = 0; i < kMaxSamples / 2; ++i) wv[i] = s[i];
+#pragma unroll
+            for (int m = 0; m < kMaxSamples; ++m)
+                if (m < c) atomicAdd(&hist[(wv[m >> 1] >> (16 * (m & 1))) & 0xffffu], 1);
         }
         __builtin_amdgcn_wave_barrier();
         __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
@@ -874,9 +891,11 @@ void launch_region_voting(RefineBufs& B, const uint32_t* arms0, int hf, const De
     hipLaunchKernelGGL(k_scan_blocks, dim3(1), dim3(SC_THREADS), 0, st, B.bsum, nb, B.counts); trace_point("k_scan_blocks", st);
     hipLaunchKernelGGL(k_scan_scatter, dim3(nb), dim3(SC_THREADS), 0, st, B.flags, n, B.bsum,
                        B.out_pos, B.out_list, B.hi_list); trace_point("k_scan_scatter", st);
+    hipLaunchKernelGGL(k_rank_samples, dim3((n + 255) / 256), dim3(256), 0, st, B.out_list, B.counts, B.vote,
+                       B.samples, B.cvote, B.csamp); trace_point("k_rank_samples", st);
     const size_t lds = (size_t)(VD_THREADS / 64) * P.L * sizeof(int);
     hipLaunchKernelGGL(k_vote_decide, dim3(1024), dim3(VD_THREADS), lds, st, B.dm, B.dtmp, arms0,
-                       B.vote, B.samples, B.out_pos, B.out_list, B.hi_list, B.counts, hf, P); trace_point("k_vote_decide", st);
+                       B.vote, B.samples, B.out_pos, B.cvote, B.csamp, B.hi_list, B.counts, hf, P); trace_point("k_vote_decide", st);
     std::swap(B.dm, B.dtmp);
 }
 

@@ -64,6 +64,8 @@ struct RefineBufs {
     int32_t* out_pos; // [H][W]
     int32_t* out_list;// [H][W]
     int32_t* hi_list; // [H][W]
+    int32_t* cvote;   // [H][W] vote count by outlier rank (out_pos order)
+    uint16_t* csamp;  // [H][W][20] low-vote samples by outlier rank
     int32_t* bsum;    // scan block sums [2 * nblocks]
     int32_t* counts;  // [4]
     uint8_t* gray;    // [H][W]
