@@ -500,12 +500,22 @@ int run_pipeline(tsm_adc* h, Workspace* w, const uint8_t* d_left, const uint8_t*
     if (dump && dump->cost_agg && (rc = dump_vol(dump->cost_agg, 2)) != TSM_OK) return rc;
     // --- scanline, then WTA of both final volumes --------------------------------------
     const bool keep_view1 = dump && dump->cost_scan;
-    if (launch_scan_vertical(w->vol, w->gv, w->img, +1, w->infvec, P, st) != 0 ||
-        launch_scan_vertical(w->vol, w->gv, w->img, -1, w->infvec, P, st) != 0 ||
-        launch_scan_horizontal(w->vol, w->gh, w->img, +1, nullptr, 1, w->infvec, P, st) != 0 ||
-        launch_scan_horizontal(w->vol, w->gh, w->img, -1, nullptr, 1, w->infvec, P, st) != 0 ||
-        launch_wta(w->vol, w->rb.disp0, w->infvec, P, st) != 0)
-        return fail(h, TSM_ERR_UNSUPPORTED, "scanline: label count");
+    // WTA: fused into the leftward pass (which then never stores view 1's final volume,
+    // only its argmin is used) or, TSM_WTA_FUSED=0, its own launch over both volumes
+    static const bool wta_fused = [] {
+        const char* e = getenv("TSM_WTA_FUSED");
+        return !(e && e[0] == '0');
+    }();
+    bool ok = launch_scan_vertical(w->vol, w->gv, w->img, +1, w->infvec, P, st) == 0 &&
+              launch_scan_vertical(w->vol, w->gv, w->img, -1, w->infvec, P, st) == 0 &&
+              launch_scan_horizontal(w->vol, w->gh, w->img, +1, nullptr, 1, w->infvec, P, st) == 0;
+    if (ok && wta_fused)
+        ok = launch_scan_horizontal(w->vol, w->gh, w->img, -1, w->rb.disp0, keep_view1 ? 1 : 0, w->infvec, P,
+                                    st) == 0;
+    else if (ok)
+        ok = launch_scan_horizontal(w->vol, w->gh, w->img, -1, nullptr, 1, w->infvec, P, st) == 0 &&
+             launch_wta(w->vol, w->rb.disp0, w->infvec, P, st) == 0;
+    if (!ok) return fail(h, TSM_ERR_UNSUPPORTED, "scanline: label count");
     mark();
     if (keep_view1 && (rc = dump_vol(dump->cost_scan, 2)) != TSM_OK) return rc;
     if (dump && dump->wta && (rc = d2h(dump->wta, w->rb.disp0, 2 * N * 4)) != TSM_OK) return rc;
