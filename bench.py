@@ -40,7 +40,7 @@ def parse():
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--batch", type=int, default=8, help="pairs per GPU per step")
-    ap.add_argument("--concurrency", type=int, default=4, help="pair pipelines in flight per GPU")
+    ap.add_argument("--concurrency", type=int, default=8, help="pair pipelines in flight per GPU")
     ap.add_argument("--height", type=int, default=375)
     ap.add_argument("--width", type=int, default=1242)
     ap.add_argument("--max-disparity", type=int, default=192)
