@@ -188,6 +188,9 @@ __global__ void k_census_desc(const uint32_t* __restrict__ img, uint32_t* __rest
 struct F3 {  // 12-B store (global_store_dwordx3; an ext_vector of 3 would claim 16-B alignment)
     float a, b, c;
 };
+struct F5 {  // 20-B store of E = 5 lanes
+    float a, b, c, d, e;
+};
 constexpr int CW_THREADS = 256;   // 4 independent waves per workgroup (tables shared)
 constexpr int CW_LUTB = 192;      // lutB slot (188 used); padding entries follow it
 constexpr int CW_CHUNK = 16;      // staging granule: 16 records x 64 B = one LDS-DMA per wave
@@ -227,7 +230,7 @@ __device__ unsigned long long g_stamps[65536 * 8];
 enum { CW_BOTH = 0, CW_VIEW0 = 1, CW_VIEW1 = 2, CW_SHEAR = 3 };
 
 template <int E, bool HSI, bool MASK, int MODE>
-__global__ __launch_bounds__(CW_THREADS) __attribute__((amdgpu_waves_per_eu(E == 3 ? 4 : 1))) void k_cost_walk(
+__global__ __launch_bounds__(CW_THREADS) __attribute__((amdgpu_waves_per_eu(E == 3 ? 4 : (E == 4 ? 3 : 1)))) void k_cost_walk(
     const uint32_t* __restrict__ desc, const float* __restrict__ lutA, int lutA_n,
     const float* __restrict__ lutB, float* __restrict__ vol, DevParams Pk, int seg_len, int nseg,
     uint32_t* __restrict__ ctr, uint32_t ctr_base) {
@@ -454,6 +457,15 @@ __global__ __launch_bounds__(CW_THREADS) __attribute__((amdgpu_waves_per_eu(E ==
                 o3.c = c[2];
                 *reinterpret_cast<F3*>(orow + (size_t)j * Lp) = o3;
             }
+            if constexpr (E == 5) {  // labels 5l .. 5l+4: 20 B per lane, 1280 B a pixel
+                F5 o5;
+                o5.a = c[0];
+                o5.b = c[1];
+                o5.c = c[2];
+                o5.d = c[3];
+                o5.e = c[4];
+                *reinterpret_cast<F5*>(orow + (size_t)j * Lp) = o5;
+            }
 #pragma unroll
             for (int q = 0; q < E / 4; ++q)
                 if (E * lane + 4 * q < Lp)
@@ -509,44 +521,53 @@ __global__ __launch_bounds__(CW_THREADS) __attribute__((amdgpu_waves_per_eu(E ==
         if (v == 0) walk(IC<0>{});
         else walk(IC<1>{});
     }
-    // E = 3 covers labels 0..191; labels 192..Lp-1 (label 192 real at L = 193, the rest
-    // +inf padding) are the tail float4 of each pixel vector: lane l computes pixel
-    // x_lo + l of the unit from global records (one gather per unit, L2-resident)
-    if constexpr (E == 3) {
-        if (Lp > 192 && lane < count0) {
-            const int k = 192;
+    // Lp = 64 E + 4 (E = 3: 193..196 labels, 4: 257..260, 5: 321..324): the lanes cover
+    // labels 0 .. 64E-1, the pixel vector's last float4 (labels 64E .. Lp-1, the real ones
+    // < L, the rest +inf padding) is the tail: lane l computes pixel x_lo + l of the unit
+    // from global records (one gather per label, L2-resident)
+    if constexpr (E == 3 || E == 4 || E == 5) {
+        if (Lp > 64 * E && lane < count0) {
             const int j = x_lo + lane;
-            uint32_t Fr[NW], Vr[NW];
+            const float inf = __int_as_float(0x7f800000);
+            uint32_t Fr[NW];
             const u32x4* rf = reinterpret_cast<const u32x4*>(dF + (size_t)clampx(j + foff) * 16);
-            const u32x4* rv = reinterpret_cast<const u32x4*>(dV + (size_t)clampx(v == 0 ? j - k : j + k) * 16);
             pick(rf[0], rf[1], rf[2], rf[3], Fr);
-            pick(rv[0], rv[1], rv[2], rv[3], Vr);
-            uint32_t cen = 0;
-            if (!HSI) {
-#pragma unroll
-                for (int w = 0; w < 6; ++w) cen = bcnt_acc((Fr[w] & Vr[6 + w]) | (Fr[6 + w] & Vr[w]), cen);
-            } else {
-                cen = __builtin_popcount(~(Fr[0] & Vr[0])) + __builtin_popcount(~(Fr[1] & Vr[1]) & vmask_hi);
-#pragma unroll
-                for (int w = 2; w < 6; ++w) cen += __builtin_popcount((Fr[w] & Vr[4 + w]) | (Fr[4 + w] & Vr[w]));
-            }
-            const uint32_t vc = Vr[NW - 1], fc = Fr[NW - 1];
-            int ai;
-            if (!HSI) {
-                ai = (int)__builtin_amdgcn_sad_u8(fc, vc, 0u);
-            } else {
-                const int hd = (int)__builtin_amdgcn_sad_u8(fc & 0xffu, vc & 0xffu, 0u);
-                ai = 2 * min(hd, 255 - hd) + 5 * (int)__builtin_amdgcn_sad_u8(fc & 0xffff00u, vc & 0xffff00u, 0u);
-            }
-            float c = 2.f - sA[ai] - sB[cen];
             const int xf = j + foff;
             const bool fixed_ok = !rowOut && xf - hw >= 0 && xf + hw < W;
             const int klo = v == 0 ? j - (W - 1 - hw) : hw - j;
             const int khi = v == 0 ? j - hw : W - 1 - hw - j;
-            c = (fixed_ok && k >= klo && k <= khi) || k >= L ? c : 2.f;
-            if (k >= L) c = __int_as_float(0x7f800000);
-            const float inf = __int_as_float(0x7f800000);
-            *reinterpret_cast<f32x4*>(vol + (((size_t)v * H + y) * W + j) * Lp + 192) = f32x4{c, inf, inf, inf};
+            float c4[4];
+#pragma unroll
+            for (int t = 0; t < 4; ++t) {
+                const int k = 64 * E + t;
+                c4[t] = inf;
+                if (k < L) {
+                    uint32_t Vr[NW];
+                    const u32x4* rv = reinterpret_cast<const u32x4*>(dV + (size_t)clampx(v == 0 ? j - k : j + k) * 16);
+                    pick(rv[0], rv[1], rv[2], rv[3], Vr);
+                    uint32_t cen = 0;
+                    if (!HSI) {
+#pragma unroll
+                        for (int w = 0; w < 6; ++w) cen = bcnt_acc((Fr[w] & Vr[6 + w]) | (Fr[6 + w] & Vr[w]), cen);
+                    } else {
+                        cen = __builtin_popcount(~(Fr[0] & Vr[0])) + __builtin_popcount(~(Fr[1] & Vr[1]) & vmask_hi);
+#pragma unroll
+                        for (int w = 2; w < 6; ++w) cen += __builtin_popcount((Fr[w] & Vr[4 + w]) | (Fr[4 + w] & Vr[w]));
+                    }
+                    const uint32_t vc = Vr[NW - 1], fc = Fr[NW - 1];
+                    int ai;
+                    if (!HSI) {
+                        ai = (int)__builtin_amdgcn_sad_u8(fc, vc, 0u);
+                    } else {
+                        const int hd = (int)__builtin_amdgcn_sad_u8(fc & 0xffu, vc & 0xffu, 0u);
+                        ai = 2 * min(hd, 255 - hd) + 5 * (int)__builtin_amdgcn_sad_u8(fc & 0xffff00u, vc & 0xffff00u, 0u);
+                    }
+                    const float c = 2.f - sA[ai] - sB[cen];
+                    c4[t] = (fixed_ok && k >= klo && k <= khi) ? c : 2.f;
+                }
+            }
+            *reinterpret_cast<f32x4*>(vol + (((size_t)v * H + y) * W + j) * Lp + 64 * E) =
+                f32x4{c4[0], c4[1], c4[2], c4[3]};
         }
     }
     CW_STAMP(3);
@@ -702,7 +723,8 @@ int launch_cost_volume(const uint32_t* img, const uint32_t* desc, const float* l
         return e && e[0] == '1';
     }();
     if (!e4 && !P.mask && (P.Lp == 192 || P.Lp == 196)) { CASE(3) }
-    else if (P.Lp <= 256) { CASE(4) }
+    else if (!e4 && !P.mask && (P.Lp == 320 || P.Lp == 324)) { CASE(5) }
+    else if (P.Lp <= 256 || (!P.mask && P.Lp == 260)) { CASE(4) }
     else if (P.Lp <= 512) { CASE(8) }
     else return -1;
 #undef CASE

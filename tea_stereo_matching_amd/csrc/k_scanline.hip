@@ -129,9 +129,11 @@ struct LaneAddr {
 };
 
 // Buffer resources of the byte maps / image; offsets are 32-bit (checked by the launcher).
+constexpr int SC_GBIAS = 512;  // >= 4 * (max label vectors = 128): no negative buffer offset
+
 struct ScanRes {
     __amdgpu_buffer_rsrc_t own;   // own-view colour differences (d1)
-    __amdgpu_buffer_rsrc_t oth;   // other view's colour differences (d2), based 256 B low
+    __amdgpu_buffer_rsrc_t oth;   // other view's colour differences (d2), based SC_GBIAS B low
     __amdgpu_buffer_rsrc_t im;    // own-view image (mask mode)
 };
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t scan_rsrc(const void* p) {
@@ -142,7 +144,8 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t scan_rsrc(const void* p) {
 // pointer; d1, the mask colour and the d2 window are buffer loads whose offsets are
 // scalar (uniform) plus, for d2, a per-lane constant: no per-step address arithmetic.
 //   d2 window of lane q: aligned byte (x0 + gb) & ~3 = S + V with S = (x0 [- 3]) & ~3
-//   (scalar) and V = +4q (view 0) or -4q (view 1); the rsrc sits 256 B low so V + 256 >= 0.
+//   (scalar) and V = +4q (view 0) or -4q (view 1); the rsrc sits SC_GBIAS B low so
+//   V + SC_GBIAS >= 0 for every label vector q < 128 (J = 2).
 template <int J, bool HORIZ, bool MASK>
 __device__ __forceinline__ void scan_issue(StepIn<J>& s, int pos, int dir, int line,
                                            const float* const (&pv)[J], const uint32_t (&gv)[J],
@@ -261,7 +264,7 @@ __global__ __launch_bounds__(256) void k_scan_line(float* __restrict__ vol,
     const int sgn = v == 0 ? 1 : -1;
     ScanRes R;
     R.own = scan_rsrc(grad + (size_t)v * H * C.gstride);
-    R.oth = scan_rsrc(grad + (size_t)(1 - v) * H * C.gstride - 256);
+    R.oth = scan_rsrc(grad + (size_t)(1 - v) * H * C.gstride - SC_GBIAS);
     R.im = scan_rsrc(img + (size_t)v * H * W);
     const uint32_t orow = HORIZ ? (uint32_t)line * (uint32_t)C.gstride : 0u;  // row offset in both maps
     const bool rev = sgn < 0;
@@ -276,14 +279,14 @@ __global__ __launch_bounds__(256) void k_scan_line(float* __restrict__ vol,
     // reads x ascending, view 1 descending (byte-reversed); + sh * 0x01010101 per step
     const uint32_t psel0 = rev ? 0x00010203u : 0x03020100u;
     LaneAddr<J> la;
-    uint32_t gv[J];  // d2 lane offsets (+256: the rsrc sits 256 B low)
+    uint32_t gv[J];  // d2 lane offsets (+SC_GBIAS: the rsrc sits that low)
 #pragma unroll
     for (int j = 0; j < J; ++j) {
         const int q = lane + 64 * j;
         const bool in = q < C.Q;
         la.vb[j] = in ? base + 4 * q : infvec;
         la.ves[j] = in ? es : 0;
-        gv[j] = (uint32_t)(256 + (in ? (sgn > 0 ? 4 * q : -4 * q) : 0));
+        gv[j] = (uint32_t)(SC_GBIAS + (in ? (sgn > 0 ? 4 * q : -4 * q) : 0));
     }
 
     f32x4 q[J];

@@ -106,3 +106,13 @@ def make_scene(seed: int, height: int, width: int, num_labels: int, n_rects: int
 def config_b(seed: int = 1000):
     """1242x375, setMinMaxDisparity(0, 192) -> 193 labels."""
     return make_scene(seed, 375, 1242, 193)
+
+
+def config_c(seed: int = 2000):
+    """1500x1000, setMinMaxDisparity(0, 256) -> 257 labels."""
+    return make_scene(seed, 1000, 1500, 257)
+
+
+def config_e(seed: int = 3000):
+    """2048x1536 grey replicated to BGR, setMinMaxDisparity(0, 320)."""
+    return make_scene(seed, 1536, 2048, 321, grayscale=True)

@@ -92,6 +92,13 @@ WIDE = [
     (33, 20, 270, 0, 188, 0),
     (34, 22, 290, 0, 192, 1),
     (35, 18, 260, 3, 195, 0),
+    # past 256 labels (configs C and E): four / five labels a lane + the tail float4 in the
+    # cost walk, two label vectors a lane in the scanline and the aggregation
+    (36, 24, 300, 0, 256, 0),
+    (37, 20, 340, 0, 320, 0),
+    (38, 22, 310, 0, 256, 1),
+    (39, 20, 300, 0, 258, 0),   # tail float4 with three real labels (257..259)
+    (40, 18, 360, 0, 323, 0),   # E = 5 lanes + a full tail (labels 320..323)
 ]
 
 
@@ -266,3 +273,20 @@ def test_census_7x5_window(matcher, tsm, oracle):
     assert np.array_equal(d_g, d_o)
     matcher.setMatchingStrategy(tsm.ColorModel.RGB)  # resets the parameter set
     assert matcher.params().census_win == 0
+
+
+@pytest.mark.parametrize("cfg", ["C", "E"])
+def test_full_size_configs_bit_exact(matcher, tsm, cfg):
+    """Configs C (1500x1000, D=[0,256]) and E (2048x1536 grey, D=[0,320]) at full size:
+    the SHA-256 of the final fp32 disparity equals the oracle's, recorded by
+    tests/golden/make_config_hashes.py (its oracle runs take minutes)."""
+    import hashlib
+    import json
+
+    gold = json.load(open(os.path.join(GOLDEN, "config_hashes.json")))[cfg]
+    left, right, _ = tsm.synthetic.config_c() if cfg == "C" else tsm.synthetic.config_e()
+    d_g, _ = _gpu(matcher, tsm, left, right, 0, 0, gold["max_disparity"])
+    d_g = np.ascontiguousarray(d_g, dtype=np.float32)
+    assert list(d_g.shape) == gold["shape"]
+    assert abs(float((d_g >= 0).mean()) - gold["valid_fraction"]) < 1e-12
+    assert hashlib.sha256(d_g.tobytes()).hexdigest() == gold["sha256"]
