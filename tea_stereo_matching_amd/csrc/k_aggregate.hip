@@ -720,6 +720,8 @@ struct AggStream {
     const int32_t* ws;     // window sizes of the dividing pass (nullptr: no divide)
     const uint32_t* pk;    // split streamer: packed descriptors of this direction, view 0
     const float* rcp;      // split streamer: reciprocals of this direction, view 0
+    int qtot;              // split streamer: label vectors per pixel (Lp / 4)
+    int qn0;               // split streamer: label vectors of slice 0 (blockIdx.y; = qtot if one slice)
     int horizontal;
     int n;                 // pixels per line
     int cpl;               // chunks per line
@@ -1056,12 +1058,17 @@ constexpr int AX_MC = 12;  // meta ring chunks (B reads chunk s - LAG + 1 before
 static_assert(AX_D == AS_RC1 && AX_D == AS_RC2 && AX_D == AX_MC, "ring slots are compile-time per unrolled step");
 static_assert(AS_AHEAD + AS_LAG <= AX_MC, "meta ring too short for the B lag");
 
-template <bool FUSED, int QT>
+// BIG: volumes of 2 GiB and more (configs C, E): vector loads through 64-bit addresses
+// instead of 32-bit buffer offsets.  Label slices: past 64 label vectors a pixel, blockIdx.y
+// picks one of two slices of the label axis (independent sums), each a narrower ring.
+template <bool FUSED, int QT, bool BIG>
 __global__ __launch_bounds__(AX_THREADS) void k_agg_split(AggStream S, DevParams Pk) {
     const DevParams P = Pk;
     extern __shared__ __attribute__((aligned(16))) f32x4 smem_f4[];
     const int H = P.H, W = P.W, Lp = P.Lp;
-    const int Q = QT > 0 ? QT : Lp >> 2;
+    const int slice = blockIdx.y;
+    const int Q = QT > 0 ? QT : (slice == 0 ? S.qn0 : S.qtot - S.qn0);
+    float* const volq = S.vol + 4 * (slice == 0 ? 0 : S.qn0);  // this slice's first label
     const uint32_t Qs = (uint32_t)Q * 16;                                // bytes per ring pixel
     const size_t vstride = (size_t)H * W * Lp;
     const size_t es = S.horizontal ? (size_t)Lp : (size_t)W * Lp;         // floats per pixel step
@@ -1137,7 +1144,7 @@ __global__ __launch_bounds__(AX_THREADS) void k_agg_split(AggStream S, DevParams
     if (roleA) {
         // ---- A: staging ring, land, pass A ----------------------------------------------
         const int lanec = lane < Q ? lane : Q - 1;
-        const __amdgpu_buffer_rsrc_t rs_vol = make_rsrc(S.vol), rs_pk = make_rsrc(S.pk),
+        const __amdgpu_buffer_rsrc_t rs_vol = make_rsrc(volq), rs_pk = make_rsrc(S.pk),
                                      rs_rcp = make_rsrc(S.rcp);
         const uint32_t voff = (uint32_t)lanec * 16;
         const uint32_t es4 = (uint32_t)(es * 4), aes4 = (uint32_t)(aes * 4);
@@ -1148,10 +1155,12 @@ __global__ __launch_bounds__(AX_THREADS) void k_agg_split(AggStream S, DevParams
         // issue position (chunk ci = s + AHEAD + AX_D at step s), advanced one chunk a step
         int il = 0, icc = 0;
         uint32_t iv = 0, ia = 0;  // byte offsets of line il: vol, descriptors (= reciprocals)
+        const float* ivp = volq;   // BIG: line il's first pixel
         auto set_line = [&]() {
             const int gl = g + il * G;
             const int v = gl / S.nlv, line = gl - v * S.nlv;
-            iv = (uint32_t)(((size_t)v * vstride + (size_t)line * ls) * 4);
+            if (BIG) ivp = volq + (size_t)v * vstride + (size_t)line * ls;
+            else iv = (uint32_t)(((size_t)v * vstride + (size_t)line * ls) * 4);
             ia = (uint32_t)(2 * v * H * W + line * (int)als) * 4;  // per-view stride 2HW
         };
         set_line();
@@ -1160,7 +1169,10 @@ __global__ __launch_bounds__(AX_THREADS) void k_agg_split(AggStream S, DevParams
         auto issue = [&](int k) {  // chunk at (il, icc) -> slot k; past the end: re-read the last pixel
             const bool past = il >= my_lines;
             const uint32_t pos = past ? (uint32_t)(S.n - 1) : (uint32_t)min(icc * AS_SEG + w, S.n - 1);
-            rv[k] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rs_vol, voff, iv + pos * es4, 0));
+            if (BIG)
+                rv[k] = *reinterpret_cast<const f32x4*>(ivp + (size_t)pos * es + 4 * lanec);
+            else
+                rv[k] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rs_vol, voff, iv + pos * es4, 0));
             rma[k] = (uint32_t)__builtin_amdgcn_raw_buffer_load_b32(rs_pk, vzero, ia + pos * aes4, 0);
             rmy[k] = S.ws ? (uint32_t)__builtin_amdgcn_raw_buffer_load_b32(rs_rcp, vzero, ia + pos * aes4, 0) : vzero;
             if (!past && ++icc == S.cpl) {
@@ -1274,7 +1286,7 @@ __global__ __launch_bounds__(AX_THREADS) void k_agg_split(AggStream S, DevParams
                 if (ob.cc * AS_SEG + w < S.n) {
                     const f32x4 acc = FUSED ? window(b_off, b_len, r2_off, r2_end)
                                             : *reinterpret_cast<const f32x4*>(lds + r2r + lane16);
-                    if (vl) *reinterpret_cast<f32x4*>(S.vol + ob.off + 4 * lane) = acc;
+                    if (vl) *reinterpret_cast<f32x4*>(volq + ob.off + 4 * lane) = acc;
                 }
                 out_step(ob);
             }
@@ -1304,26 +1316,32 @@ static void agg_stream_attrs() {
     (void)hipFuncSetAttribute((const void*)k_agg_stream<FUSED, 49>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
 }
 
+template <bool FUSED, int QT, bool BIG>
+static void launch_split_t(const AggStream& S, const DevParams& P, dim3 grid, size_t lds, hipStream_t st) {
+    static bool attr = false;
+    if (!attr) {
+        (void)hipFuncSetAttribute((const void*)k_agg_split<FUSED, QT, BIG>,
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+        attr = true;
+    }
+    hipLaunchKernelGGL((k_agg_split<FUSED, QT, BIG>), grid, dim3(AX_THREADS), lds, st, S, P);
+}
+
 // Returns -1 if the streamer does not support the geometry (caller falls back).
 int launch_agg_stream(float* vol, const uint32_t* arms, const int32_t* ws, const int32_t* ws_base,
                       int horizontal, bool fused, const DevParams& P, hipStream_t st) {
     const int Q = P.Lp / 4;
-    if (Q > 64 || P.max_length1 - 1 > AS_MAX_ARM) return -1;
-    if ((size_t)2 * P.H * P.W * P.Lp * 4 >= ((size_t)1 << 31)) return -1;  // 32-bit buffer offsets
-    const size_t lds = agg_stream_lds(P, fused);
-    if (lds > 160 * 1024) return -1;
-    static bool attr_set = false;
-    if (!attr_set) {
-        agg_stream_attrs<false>();
-        agg_stream_attrs<true>();
-        attr_set = true;
-    }
+    if (Q > 128 || P.max_length1 - 1 > AS_MAX_ARM) return -1;
+    const bool big = (size_t)2 * P.H * P.W * P.Lp * 4 >= ((size_t)1 << 31);  // past 32-bit offsets
     AggStream S;
     S.vol = vol;
     S.arms = arms;
     S.ws = ws;
     S.rcp = reinterpret_cast<const float*>(ws_base + (size_t)(4 + horizontal) * P.H * P.W);
     S.pk = reinterpret_cast<const uint32_t*>(ws_base + (size_t)(8 + horizontal) * P.H * P.W);
+    S.qtot = Q;
+    S.qn0 = Q > 64 ? (Q + 1) / 2 : Q;  // past 64 label vectors: two slices (blockIdx.y)
+    const int nslice = Q > 64 ? 2 : 1;
     S.horizontal = horizontal;
     S.n = horizontal ? P.W : P.H;
     S.cpl = (S.n + AS_SEG - 1) / AS_SEG;
@@ -1336,34 +1354,39 @@ int launch_agg_stream(float* vol, const uint32_t* arms, const int32_t* ws, const
         return n > 0 ? n : 256;
     }();
     const int G = S.nl < ncu ? S.nl : ncu;
-    // fused pairs: the role-split v6 (368 vs 377 us on config B); single passes: v5 (286 vs
-    // 316 us).  TSM_AGG_KERNEL=stream forces v5, =split v6 for both.
+    // fused pairs: the role-split v6; single passes: v5 (both sliced / big volumes: v6).
+    // TSM_AGG_KERNEL=stream forces v5 where it fits, =split v6 for both.
     static const int pick = [] {
         const char* e = getenv("TSM_AGG_KERNEL");
         return !e ? 0 : (e[0] == 's' && e[1] == 't') ? 1 : (e[0] == 's' && e[1] == 'p') ? 2 : 0;
     }();
-    const bool split = pick == 2 || (pick == 0 && fused);
-    if (split && agg_split_lds(P) <= 160 * 1024) {
-        static bool split_attr = false;
-        if (!split_attr) {
-            (void)hipFuncSetAttribute((const void*)k_agg_split<false, 0>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-            (void)hipFuncSetAttribute((const void*)k_agg_split<false, 49>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-            (void)hipFuncSetAttribute((const void*)k_agg_split<true, 0>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-            (void)hipFuncSetAttribute((const void*)k_agg_split<true, 49>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-            split_attr = true;
-        }
-        const size_t slds = agg_split_lds(P);
-        const dim3 sgrid(G), sblock(AX_THREADS);
+    const bool v5_fits = Q <= 64 && !big && agg_stream_lds(P, fused) <= 160 * 1024;
+    const bool split = pick == 2 || (pick == 0 && fused) || !v5_fits;
+    if (split) {
+        const int qs = S.qn0;  // the widest slice
+        const size_t slds = ((size_t)AS_RP1 + AS_RP2 + 2 * AX_MIR) * qs * 16 + (size_t)AX_MC * AS_SEG * AX_MW * 4;
+        if (slds > 160 * 1024) return -1;
+        (void)agg_split_lds;
+        const dim3 sgrid(G, nslice);
         if (fused) {
-            if (Q == 49) hipLaunchKernelGGL((k_agg_split<true, 49>), sgrid, sblock, slds, st, S, P);
-            else hipLaunchKernelGGL((k_agg_split<true, 0>), sgrid, sblock, slds, st, S, P);
+            if (Q == 49) launch_split_t<true, 49, false>(S, P, sgrid, slds, st);
+            else if (big) launch_split_t<true, 0, true>(S, P, sgrid, slds, st);
+            else launch_split_t<true, 0, false>(S, P, sgrid, slds, st);
         } else {
-            if (Q == 49) hipLaunchKernelGGL((k_agg_split<false, 49>), sgrid, sblock, slds, st, S, P);
-            else hipLaunchKernelGGL((k_agg_split<false, 0>), sgrid, sblock, slds, st, S, P);
+            if (Q == 49) launch_split_t<false, 49, false>(S, P, sgrid, slds, st);
+            else if (big) launch_split_t<false, 0, true>(S, P, sgrid, slds, st);
+            else launch_split_t<false, 0, false>(S, P, sgrid, slds, st);
         }
         trace_point(fused ? "k_agg_split<fused>" : "k_agg_split", st);
         return 0;
     }
+    static bool attr_set = false;
+    if (!attr_set) {
+        agg_stream_attrs<false>();
+        agg_stream_attrs<true>();
+        attr_set = true;
+    }
+    const size_t lds = agg_stream_lds(P, fused);
     const dim3 grid(G), block(AS_THREADS);
     if (fused) {
         if (Q == 49) hipLaunchKernelGGL((k_agg_stream<true, 49>), grid, block, lds, st, S, P);
