@@ -1369,12 +1369,12 @@ int launch_agg_stream(float* vol, const uint32_t* arms, const int32_t* ws, const
         (void)agg_split_lds;
         const dim3 sgrid(G, nslice);
         if (fused) {
-            if (Q == 49) launch_split_t<true, 49, false>(S, P, sgrid, slds, st);
-            else if (big) launch_split_t<true, 0, true>(S, P, sgrid, slds, st);
+            if (big) launch_split_t<true, 0, true>(S, P, sgrid, slds, st);
+            else if (Q == 49) launch_split_t<true, 49, false>(S, P, sgrid, slds, st);
             else launch_split_t<true, 0, false>(S, P, sgrid, slds, st);
         } else {
-            if (Q == 49) launch_split_t<false, 49, false>(S, P, sgrid, slds, st);
-            else if (big) launch_split_t<false, 0, true>(S, P, sgrid, slds, st);
+            if (big) launch_split_t<false, 0, true>(S, P, sgrid, slds, st);
+            else if (Q == 49) launch_split_t<false, 49, false>(S, P, sgrid, slds, st);
             else launch_split_t<false, 0, false>(S, P, sgrid, slds, st);
         }
         trace_point(fused ? "k_agg_split<fused>" : "k_agg_split", st);
