@@ -2,8 +2,9 @@
 """Golden hashes for SURVEY §8 configs C and E at full size (test infrastructure).
 
 Runs the oracle (oracle/, the C restatement of source/ADCensus.cpp) on the synthetic
-config C pair (1500x1000, setMinMaxDisparity(0, 256)) and config E pair (2048x1536 grey
-replicated to BGR, setMinMaxDisparity(0, 320)), serial scanline semantics, RGB model,
+config C pair (1500x1000, setMinMaxDisparity(0, 256)), config E pair (2048x1536 grey
+replicated to BGR, setMinMaxDisparity(0, 320)) and a 2400x1600 pair at D=[0,192] (a volume
+past 2 GiB at config B's label count), serial scanline semantics, RGB model,
 and records the SHA-256 of the fp32 disparity bytes plus a few statistics in
 tests/golden/config_hashes.json.  The GPU test compares its own output's hash: a
 bit-exact check at sizes whose oracle run takes minutes (too long for the GPU suite).
@@ -29,9 +30,16 @@ from oracle import oracle as O  # noqa: E402
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--threads", type=int, default=os.cpu_count() or 1)
+    ap.add_argument("--only", nargs="*", default=None, help="subset of C, E, BIG49 (others kept)")
     args = ap.parse_args()
-    out = {}
-    for name, gen, D in (("C", syn.config_c, 256), ("E", syn.config_e, 320)):
+    path = os.path.join(ROOT, "tests", "golden", "config_hashes.json")
+    out = json.load(open(path)) if os.path.exists(path) else {}
+    cases = (("C", syn.config_c, 256), ("E", syn.config_e, 320),
+             # a 6 GB volume at config B's 193 labels: the 64-bit-address aggregation path
+             ("BIG49", lambda: syn.make_scene(4000, 1600, 2400, 193), 192))
+    for name, gen, D in cases:
+        if args.only and name not in args.only:
+            continue
         left, right, _ = gen()
         t0 = time.time()
         d, _ = O.compute(left, right, O.default_params(O.RGB, 0, D, num_threads=args.threads))
@@ -44,7 +52,7 @@ def main():
             "oracle_seconds": round(time.time() - t0, 1), "oracle_threads": args.threads,
         }
         print(name, out[name], flush=True)
-    with open(os.path.join(ROOT, "tests", "golden", "config_hashes.json"), "w") as f:
+    with open(path, "w") as f:
         json.dump(out, f, indent=1)
 
 

@@ -275,16 +275,19 @@ def test_census_7x5_window(matcher, tsm, oracle):
     assert matcher.params().census_win == 0
 
 
-@pytest.mark.parametrize("cfg", ["C", "E"])
+@pytest.mark.parametrize("cfg", ["C", "E", "BIG49"])
 def test_full_size_configs_bit_exact(matcher, tsm, cfg):
-    """Configs C (1500x1000, D=[0,256]) and E (2048x1536 grey, D=[0,320]) at full size:
-    the SHA-256 of the final fp32 disparity equals the oracle's, recorded by
+    """Configs C (1500x1000, D=[0,256]) and E (2048x1536 grey, D=[0,320]) at full size, and
+    a 2400x1600 D=[0,192] pair (a 6 GB volume: the 64-bit aggregation path at 49 label
+    vectors): the SHA-256 of the final fp32 disparity equals the oracle's, recorded by
     tests/golden/make_config_hashes.py (its oracle runs take minutes)."""
     import hashlib
     import json
 
     gold = json.load(open(os.path.join(GOLDEN, "config_hashes.json")))[cfg]
-    left, right, _ = tsm.synthetic.config_c() if cfg == "C" else tsm.synthetic.config_e()
+    gen = {"C": tsm.synthetic.config_c, "E": tsm.synthetic.config_e,
+           "BIG49": lambda: tsm.synthetic.make_scene(4000, 1600, 2400, 193)}[cfg]
+    left, right, _ = gen()
     d_g, _ = _gpu(matcher, tsm, left, right, 0, 0, gold["max_disparity"])
     d_g = np.ascontiguousarray(d_g, dtype=np.float32)
     assert list(d_g.shape) == gold["shape"]
