@@ -473,12 +473,11 @@ int run_pipeline(tsm_adc* h, Workspace* w, const uint8_t* d_left, const uint8_t*
             passes.push_back({hf ? 0 : 1, wsel});
             hf = !hf;
         }
-        // v5 (persistent line streamer, pairs fused) where the geometry fits; the v3 DMA
-        // streamer (one pass per launch) otherwise.  TSM_AGG_KERNEL=dma forces v3,
-        // =grp the label-grouped v4.
+        // the persistent line streamers (pairs fused) where the geometry fits; the v3 DMA
+        // streamer (one pass per launch) otherwise.  TSM_AGG_KERNEL=dma forces v3.
         static const int kind = [] {
             const char* e = getenv("TSM_AGG_KERNEL");
-            return !e ? 0 : e[0] == 'd' ? 1 : e[0] == 'g' ? 2 : 0;
+            return !e ? 0 : e[0] == 'd' ? 1 : 0;
         }();
         for (size_t i = 0; i < passes.size(); ++i) {
             const Pass& a = passes[i];
@@ -487,9 +486,6 @@ int run_pipeline(tsm_adc* h, Workspace* w, const uint8_t* d_left, const uint8_t*
             int rcp = -1;
             if (kind == 0) {
                 rcp = launch_agg_stream(w->vol, w->arms, a.ws, w->ws, a.horizontal, pair, P, st);
-                if (rcp == 0 && pair) ++i;
-            } else if (kind == 2) {
-                rcp = launch_agg_pass(w->vol, w->arms, a.ws, a.horizontal, pair, P, st);
                 if (rcp == 0 && pair) ++i;
             }
             if (rcp != 0) rcp = launch_agg_line(w->vol, w->arms, a.ws, a.horizontal, P, st);

@@ -490,174 +490,6 @@ __global__ __launch_bounds__(AGD_THREADS) void k_agg_dma(float* __restrict__ vol
 // ---------------------------------------------------------------------------
 // 1-D aggregation v4: label-grouped streamer, optionally two passes fused
 // ---------------------------------------------------------------------------
-// The label axis is cut into G groups of QG <= 16 float4 (G = ceil(Q/16)): a workgroup
-// owns one (line, group), so its LDS ring holds 4x more pixels than a full-vector ring,
-// and each summing wave computes 4 outputs at once (16 lanes each; their windows are
-// walked together, lanes past their own window add +0.0 -- exact, sums are >= +0).
-// Same-direction passes that follow each other (the 2nd pass of an iteration and the
-// 1st of the next: V,V and H,H) run FUSED: pass A's outputs (divided by the window
-// sizes) go to a second LDS ring and pass B sums them AH+1 chunks later, so the volume
-// makes one HBM round trip for two passes.  Loading as in v3 (LDS-DMA by loader waves
-// taking whole chunks in turn, counted vmcnt, bare barriers).  The AGG_G workgroups of a
-// line share one XCD (block id = line_hi*8G + g*8 + line_lo), so the 128-B lines that
-// straddle two groups are fetched once into that XCD's L2.
-constexpr int AGG_SUM = 8;                 // summing waves
-constexpr int AGG_LOAD = 2;                // loader waves
-constexpr int AGG_SEG = 4 * AGG_SUM;       // pixels per chunk = outputs per step
-constexpr int AGG_THREADS = (AGG_SUM + AGG_LOAD) * 64;
-constexpr int AGG_MAX_RING = 48;
-
-template <bool FUSED>
-__global__ __launch_bounds__(AGG_THREADS) void k_agg_grp(float* __restrict__ vol,
-                                                         const uint32_t* __restrict__ arms,
-                                                         const int32_t* __restrict__ wsA,
-                                                         int horizontal, int A, int RC1, int D,
-                                                         int G, int QG, DevParams Pk) {
-    const DevParams P = Pk;  // kernel args -> registers once (no per-use kernarg reloads)
-    extern __shared__ __attribute__((aligned(16))) f32x4 smem_f4[];
-    const int H = P.H, W = P.W, Lp = P.Lp;
-    const int Q = Lp >> 2;
-    const int n = horizontal ? W : H;
-    const int nlines = horizontal ? H : W;
-    // block -> (line, group): the G groups of a line share block id mod 8 (one XCD)
-    const int id = blockIdx.x;
-    const int line = (id / (8 * G)) * 8 + (id & 7);
-    const int g = (id >> 3) % G;
-    const int v = blockIdx.y;
-    if (line >= nlines) return;  // whole workgroup: no barrier reached
-    const int q0 = g * QG;                   // first float4 of this group
-    const int QGg = min(QG, Q - q0);         // float4 of this group (last may be short)
-    const int CS = AGG_SEG * QG;             // float4 per chunk (pixel-linear ring)
-    const int ndma = (CS + 63) >> 6;
-    const int AH = (A + AGG_SEG - 1) / AGG_SEG;
-    const int RC2 = FUSED ? 2 * AH + 2 : 0;
-    const int RP1 = RC1 * AGG_SEG, RP2 = RC2 * AGG_SEG;
-    const size_t es = horizontal ? (size_t)Lp : (size_t)W * Lp;
-    float* base = vol + (size_t)v * H * W * Lp + (horizontal ? (size_t)line * W * Lp : (size_t)line * Lp) + 4 * q0;
-    const uint32_t* ab = arms + (size_t)v * H * W + (horizontal ? (size_t)line * W : (size_t)line);
-    const size_t as = horizontal ? 1 : (size_t)W;
-    const int32_t* wsl = wsA ? wsA + (size_t)v * 2 * H * W + (horizontal ? (size_t)line * W : (size_t)line) : nullptr;
-    const int shA = horizontal ? 16 : 0, shB = horizontal ? 24 : 8;
-    f32x4* ring1 = smem_f4;
-    f32x4* ring2 = ring1 + (size_t)RC1 * CS + 4 * 16;       // + read pad
-    uint32_t* arm_s = reinterpret_cast<uint32_t*>(ring2 + (size_t)RC2 * CS + 4 * 16);
-    float* ws_s = reinterpret_cast<float*>(arm_s + n);
-
-    const int tid = threadIdx.x;
-    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-    const int lane = tid & 63;
-    const int nchunks = (n + AGG_SEG - 1) / AGG_SEG;
-    const bool loader = wave >= AGG_SUM;
-    const int li = wave - AGG_SUM;
-    const int slot_t = lane >> 4, q = lane & 15;  // output slot (of 4) and float4 in group
-
-    // loaders: chunk c (loader c % AGG_LOAD) -> ring1 slot c % RC1; DMA instruction k
-    // moves chunk float4 f = 64k + lane: pixel f / QG, group float4 f % QG (clamped to
-    // the group's data; the last instruction masks lanes past the chunk)
-    constexpr int KMAX = (AGG_SEG * 16) / 64;
-    int pxo[KMAX];
-    uint32_t gofs[KMAX];
-#pragma unroll
-    for (int k = 0; k < KMAX; ++k) {
-        const int f = k * 64 + lane;
-        const int px = f / QG;
-        const int qq = f - px * QG;
-        pxo[k] = f < CS ? px : 0;
-        gofs[k] = 4u * (uint32_t)(qq < QGg ? qq : QGg - 1);
-    }
-    const bool last_lane_ok = (ndma - 1) * 64 + lane < CS;
-    auto dma_chunk = [&](int c) {
-        if (c % AGG_LOAD != li) return;
-        f32x4* slot = ring1 + (size_t)(c % RC1) * CS;
-#pragma unroll
-        for (int k = 0; k < KMAX; ++k) {
-            if (k < ndma && (k < ndma - 1 || last_lane_ok)) {
-                int px = c * AGG_SEG + pxo[k];
-                px = px < n ? px : n - 1;
-                const float* src = base + (size_t)px * es + gofs[k];
-                __builtin_amdgcn_global_load_lds(src, slot + k * 64, 16, 0, 0);
-            }
-        }
-    };
-    const int younger = ndma * ((D - 1) / AGG_LOAD);
-    if (loader) {
-        for (int c = 0; c < AH + D; ++c) dma_chunk(c);
-    }
-    for (int i = tid; i < n; i += AGG_THREADS) {
-        const uint32_t a = ab[(size_t)i * as];
-        arm_s[i] = (((a >> shA) & 0xffu) << 16) | ((a >> shB) & 0xffu);  // lo<<16 | hi
-        if (wsl) ws_s[i] = (float)wsl[(size_t)i * as];
-    }
-    __syncthreads();  // arms / window sizes staged (full fence once)
-
-    // window sum of the 4 outputs of this wave (lane slot t: output o_t) over a pixel-
-    // linear ring of RP pixels: sequential per output, in window order
-    auto window_sum = [&](const f32x4* ring, int RP, int o, bool ok) -> f32x4 {
-        int lo = 0, len = 0;
-        if (ok) {
-            const uint32_t a = arm_s[o];
-            lo = (int)(a >> 16);
-            len = lo + (int)(a & 0xffffu) + 1;
-        }
-        int maxlen = max(max(__builtin_amdgcn_readlane(len, 0), __builtin_amdgcn_readlane(len, 16)),
-                         max(__builtin_amdgcn_readlane(len, 32), __builtin_amdgcn_readlane(len, 48)));
-        int idx = ok ? (o - lo) % RP : 0;  // ring pixel of the window start
-        f32x4 acc = f32x4{0.f, 0.f, 0.f, 0.f};
-        for (int t = 0; t < maxlen; t += 4) {
-            f32x4 x[4];
-            int ix = idx;
-#pragma unroll
-            for (int u = 0; u < 4; ++u) {
-                x[u] = ring[(size_t)ix * QG + q];
-                ix = ix + 1 == RP ? 0 : ix + 1;
-            }
-#pragma unroll
-            for (int u = 0; u < 4; ++u) {
-                const bool in = t + u < len;
-                acc.x += in ? x[u].x : 0.f;
-                acc.y += in ? x[u].y : 0.f;
-                acc.z += in ? x[u].z : 0.f;
-                acc.w += in ? x[u].w : 0.f;
-            }
-            idx = ix;
-        }
-        return acc;
-    };
-
-    const int nsteps = nchunks + (FUSED ? AH + 1 : 0);
-    for (int s = 0; s < nsteps; ++s) {
-        if (loader) wait_vmcnt(younger);          // chunk s+AH landed
-        else asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // ring2 writes of step s-1 done
-        __builtin_amdgcn_s_barrier();
-        if (loader) {
-            dma_chunk(s + AH + D);                // into the slot of chunk s-AH-1
-            continue;
-        }
-        if (s < nchunks) {  // pass A (or the single pass) on chunk s
-            const int o = s * AGG_SEG + 4 * wave + slot_t;
-            const bool ok = o < n;
-            f32x4 r = window_sum(ring1, RP1, o, ok);
-            if (wsl && ok) {
-                const float wsz = ws_s[o];
-                r /= wsz;
-            }
-            if (FUSED) {
-                if (ok && q < QG) ring2[(size_t)(o % RP2) * QG + q] = r;
-            } else if (ok && q < QGg) {
-                *reinterpret_cast<f32x4*>(base + (size_t)o * es + 4 * q) = r;
-            }
-        }
-        if (FUSED && s >= AH + 1) {  // pass B on chunk s-AH-1 (its pass-A inputs are in ring2)
-            const int o = (s - AH - 1) * AGG_SEG + 4 * wave + slot_t;
-            const bool ok = o < n;
-            const f32x4 r = window_sum(ring2, RP2, o, ok);
-            if (ok && q < QGg) *reinterpret_cast<f32x4*>(base + (size_t)o * es + 4 * q) = r;
-        }
-    }
-    if (loader) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // no DMA outlives the WG
-}
-
-// ---------------------------------------------------------------------------
 // 1-D aggregation v5: persistent line streamer, same-direction pass pairs fused
 // ---------------------------------------------------------------------------
 // Each workgroup (one per CU) owns every G-th line of the pass (both views) and treats
@@ -1399,51 +1231,6 @@ int launch_agg_stream(float* vol, const uint32_t* arms, const int32_t* ws, const
     return 0;
 }
 
-// Ring geometry of the grouped streamer: LDS bytes, ring1 chunks RC1 and DMA depth D
-// (D - 1 a multiple of the loader count), or 0 if it does not fit.
-static size_t agg_grp_geometry(const DevParams& P, bool fused, int& G, int& QG, int& RC1, int& D) {
-    const int A = P.max_length1 - 1;
-    const int Q = P.Lp / 4;
-    G = (Q + 15) / 16;
-    QG = (Q + G - 1) / G;
-    const int CS = AGG_SEG * QG;
-    const int AH = (A + AGG_SEG - 1) / AGG_SEG;
-    const int RC2 = fused ? 2 * AH + 2 : 0;
-    const int nmax = P.W > P.H ? P.W : P.H;
-    const size_t fixed = (size_t)nmax * 8 + (size_t)(RC2 * CS + 2 * 4 * 16) * 16;
-    const size_t chunk = (size_t)CS * 16;
-    if (fixed >= 160 * 1024) return 0;
-    int rc = (int)((160 * 1024 - fixed) / chunk);
-    rc = rc > AGG_MAX_RING ? AGG_MAX_RING : rc;
-    int d = rc - (2 * AH + 1);
-    d -= (d - 1) % AGG_LOAD;
-    if (d < 2) return 0;
-    RC1 = 2 * AH + 1 + d;
-    D = d;
-    return (size_t)RC1 * chunk + fixed;
-}
-
-int launch_agg_pass(float* vol, const uint32_t* arms, const int32_t* ws, int horizontal, bool fused,
-                    const DevParams& P, hipStream_t st) {
-    static bool attr_set = false;
-    if (!attr_set) {
-        (void)hipFuncSetAttribute((const void*)k_agg_grp<false>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-        (void)hipFuncSetAttribute((const void*)k_agg_grp<true>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-        attr_set = true;
-    }
-    int G, QG, RC1, D;
-    const size_t lds = agg_grp_geometry(P, fused, G, QG, RC1, D);
-    if (!lds) return -1;
-    const int A = P.max_length1 - 1;
-    const int nlines = horizontal ? P.H : P.W;
-    dim3 g(((nlines + 7) / 8) * 8 * G, 2);
-    if (fused)
-        hipLaunchKernelGGL((k_agg_grp<true>), g, dim3(AGG_THREADS), lds, st, vol, arms, ws, horizontal, A, RC1, D, G, QG, P);
-    else
-        hipLaunchKernelGGL((k_agg_grp<false>), g, dim3(AGG_THREADS), lds, st, vol, arms, ws, horizontal, A, RC1, D, G, QG, P);
-    trace_point(fused ? "k_agg_grp<fused>" : "k_agg_grp", st);
-    return 0;
-}
 
 void launch_arms(const uint32_t* img, uint32_t* arms, const DevParams& P, hipStream_t st) {
     dim3 g((P.W + 127) / 128, P.H, 2);

@@ -31,11 +31,6 @@ void launch_window_sizes(const uint32_t* arms, int32_t* ws, const DevParams& P, 
 void launch_color_grad(const uint32_t* img, uint8_t* gv, uint8_t* gh, const DevParams& P,
                        hipStream_t st);
 size_t agg_lds_bytes(const DevParams& P);
-// One 1-D pass (ws: divide by the window sizes), or -- fused -- a pass with ws followed
-// by a pass without in the same direction (the 2nd pass of an iteration + the 1st of the
-// next).  Returns -1 if the geometry does not fit.
-int launch_agg_pass(float* vol, const uint32_t* arms, const int32_t* ws, int horizontal, bool fused,
-                    const DevParams& P, hipStream_t st);
 // ws_base: the window-size workspace (ws, reciprocals, packed descriptors; k_window_sizes)
 int launch_agg_stream(float* vol, const uint32_t* arms, const int32_t* ws, const int32_t* ws_base,
                       int horizontal, bool fused, const DevParams& P, hipStream_t st);

@@ -17,6 +17,9 @@ for a in "$@"; do
     views) run views TSM_COST_VIEWS=1 ;;
     e4views) run e4views TSM_COST_VIEWS=1 TSM_COST_E4=1 ;;
     views32) run views32 TSM_COST_SEG=32 ;;
+    seg72) run seg72 TSM_COST_SEG=72 ;;
+    seg96) run seg96 TSM_COST_SEG=96 ;;
+    seg144) run seg144 TSM_COST_SEG=144 ;;
     views64) run views64 TSM_COST_SEG=64 ;;
     both) run both TSM_COST_BOTH=1 ;;
     shear) run shear TSM_COST_SHEAR=1 ;;

@@ -1,6 +1,6 @@
 #!/bin/bash
 # GPU box: parity tests (stop on failure), then a concurrency-1 kernel trace of the
-# in-tree library and, optionally, of TSM_AGG_KERNEL variants ("dma", "grp").
+# in-tree library and, optionally, of TSM_AGG_KERNEL variants ("dma", "stream", "split").
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 mkdir -p gpurun_out
