@@ -249,7 +249,17 @@ __global__ __launch_bounds__(CW_THREADS) __attribute__((amdgpu_waves_per_eu(E ==
     (void)ctr_base;
     // one walk unit (view, row, segment) per wave; the unit's loads (ring prologue and
     // warm-up gather) are issued before the table fill's barrier so their latencies overlap
-    const int gw0 = blockIdx.x * (CW_THREADS / 64) + wave;
+    // XCD-aware unit order: workgroups are dealt round-robin to the 8 XCDs, so block b runs
+    // on XCD b % 8; remapping b -> (b % 8) * per + b / 8 gives each XCD a contiguous run of
+    // units (neighbouring segments of the same rows), whose warm-up gathers and tails then
+    // re-read records its own L2 already holds.  TSM_EXP_NO_XCD keeps the linear order.
+    const int nb = gridDim.x, per = nb >> 3;
+#ifdef TSM_EXP_NO_XCD
+    const int blk = blockIdx.x;
+#else
+    const int blk = (int)blockIdx.x < 8 * per ? ((int)blockIdx.x & 7) * per + ((int)blockIdx.x >> 3) : (int)blockIdx.x;
+#endif
+    const int gw0 = blk * (CW_THREADS / 64) + wave;
     constexpr bool SHEAR = MODE == CW_SHEAR;
     const bool active = gw0 < (MODE == CW_BOTH ? 2 : 1) * H * nseg;
     const int gw = active ? gw0 : 0;
