@@ -52,14 +52,16 @@ __device__ __forceinline__ uint32_t umin3(uint32_t a, uint32_t b, uint32_t c) {
     return min(min(a, b), c);  // lowered to v_min3_u32
 }
 
-// wave min of non-negative floats held as bits (+inf padding is neutral)
-template <int J>
+// wave min of non-negative floats held as bits (+inf padding is neutral).  VG: keep it in
+// VGPRs via the gfx950 lane swaps (faster on the scanline's serial chain when every
+// consumer is a vector op; the WTA's scalar uses prefer the readlane form).
+template <int J, bool VG = false>
 __device__ __forceinline__ uint32_t vec_min_bits(const f32x4 (&x)[J]) {
     uint32_t m = min(min(fbits(x[0][0]), fbits(x[0][1])), min(fbits(x[0][2]), fbits(x[0][3])));
 #pragma unroll
     for (int j = 1; j < J; ++j)
         m = min(m, min(min(fbits(x[j][0]), fbits(x[j][1])), min(fbits(x[j][2]), fbits(x[j][3]))));
-    return wave_min_bits(m);
+    return VG ? wave_min_bits_v(m) : wave_min_bits(m);
 }
 
 // WTA over indices [minD, L-1], first minimum (strict <, ADCensus.cpp:1404): the first d
@@ -374,7 +376,7 @@ __global__ __launch_bounds__(256) void k_scan_line(float* __restrict__ vol,
                 }
 #pragma unroll
                 for (int j = 0; j < J; ++j) cur[j] += dstep[j];
-                mq = vec_min_bits<J>(q);
+                mq = vec_min_bits<J, !WTA>(q);
                 if (WTA) {
                     const int d = vec_argmin<J>(q, lane, C.L, C.minD, mq);
                     if (lane == 0) wrow[pos] = d;

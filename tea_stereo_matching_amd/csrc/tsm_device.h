@@ -105,6 +105,17 @@ __device__ __forceinline__ uint32_t wave_min_bits(uint32_t v) {
     const uint32_t r3 = __builtin_amdgcn_readlane(v, 48);
     return min(min(r0, r1), min(r2, r3));
 }
+// Same, kept in VGPRs (every lane ends with the wave min): the row minima are combined
+// by the gfx950 lane swaps v_permlane32_swap (rows 0,1 <-> 2,3) and v_permlane16_swap
+// (rows 0 <-> 1, 2 <-> 3) instead of readlanes, so a VALU consumer needs no
+// VALU -> SGPR -> VALU round trip.
+__device__ __forceinline__ uint32_t wave_min_bits_v(uint32_t v) {
+    v = dpp_row_min(v);
+    const auto a = __builtin_amdgcn_permlane32_swap(v, v, false, false);
+    v = min((uint32_t)a[0], (uint32_t)a[1]);
+    const auto b = __builtin_amdgcn_permlane16_swap(v, v, false, false);
+    return min((uint32_t)b[0], (uint32_t)b[1]);
+}
 __device__ __forceinline__ float wave_min_nonneg(float x) {
     return __uint_as_float(wave_min_bits(__float_as_uint(x)));
 }
