@@ -97,6 +97,42 @@ __device__ __forceinline__ int vec_argmin(const f32x4 (&x)[J], int lane, int L, 
     return minD;
 }
 
+// Same result, branch-free and with the minimum m held in VGPRs (every lane equal), for
+// the fused WTA inside the scanline's serial loop: no basic-block boundary per step, so
+// the compiler can interleave one step's argmin with the next step's dependent chain.
+template <int J>
+__device__ __forceinline__ int vec_argmin_nb(const f32x4 (&x)[J], int lane, int L, int minD, uint32_t m) {
+    if (minD > 0) {
+        uint32_t mm = ~0u;
+#pragma unroll
+        for (int j = 0; j < J; ++j)
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+                const int d = 4 * (lane + 64 * j) + e;
+                if (d >= minD) mm = min(mm, fbits(x[j][e]));
+            }
+        m = wave_min_bits_v(mm);
+    }
+    const bool valid = __ballot(bitsf(m) < 3.402823466e+38f) != 0;  // reference: unset otherwise
+    int res = minD;
+    bool found = false;
+#pragma unroll
+    for (int j = J - 1; j >= 0; --j) {  // descending: the lowest j that holds m wins
+        int first = 4;
+#pragma unroll
+        for (int e = 3; e >= 0; --e) {
+            const int d = 4 * (lane + 64 * j) + e;
+            if (fbits(x[j][e]) == m && d >= minD && d < L) first = e;
+        }
+        const uint64_t mask = __ballot(first < 4);
+        const int ln = mask ? (int)__builtin_ctzll(mask) : 0;
+        const int cand = 4 * (ln + 64 * j) + __builtin_amdgcn_readlane(first, ln);
+        res = mask ? cand : res;
+        found = found || mask != 0;
+    }
+    return (valid && found) ? res : minD;
+}
+
 // Hot-loop scalars, pinned in SGPRs (an empty asm makes each value opaque, so the
 // compiler cannot rematerialise it from kernarg memory inside the serial loop).
 struct ScanConst {
@@ -334,6 +370,8 @@ __global__ __launch_bounds__(256) void k_scan_line(float* __restrict__ vol,
     }
     int pfi = SC_K < n ? SC_K : n - 1;  // step index pf points at (clamped to the last)
 
+    static_assert(64 % SC_K == 0, "WTA groups of 64 steps hold whole unrolled blocks");
+    int dacc = 0;  // WTA: indices of the current group of 64 steps, one per lane
     for (int b = 0; b < n; b += SC_K) {
 #pragma unroll
         for (int k = 0; k < SC_K; ++k) {
@@ -376,11 +414,19 @@ __global__ __launch_bounds__(256) void k_scan_line(float* __restrict__ vol,
                 }
 #pragma unroll
                 for (int j = 0; j < J; ++j) cur[j] += dstep[j];
+#ifdef TSM_EXP_WTA_LANE0
                 mq = vec_min_bits<J, !WTA>(q);
                 if (WTA) {
                     const int d = vec_argmin<J>(q, lane, C.L, C.minD, mq);
                     if (lane == 0) wrow[pos] = d;
                 }
+#else
+                mq = vec_min_bits<J, true>(q);
+                if (WTA) {  // step it's index lands in lane it & 63, stored 64 steps at a time
+                    const int d = vec_argmin_nb<J>(q, lane, C.L, C.minD, mq);  // whole wave
+                    dacc = lane == (it & 63) ? d : dacc;
+                }
+#endif
                 // refill this slot only now that its data is consumed (a load into a live
                 // slot would make the compiler stage it in temporaries and copy it back,
                 // waiting for the load right away)
@@ -392,6 +438,12 @@ __global__ __launch_bounds__(256) void k_scan_line(float* __restrict__ vol,
                 }
             }
         }
+#ifndef TSM_EXP_WTA_LANE0
+        if (WTA && (((b + SC_K) & 63) == 0 || b + SC_K >= n)) {  // flush a group of 64 steps
+            const int g0 = b & ~63;
+            if (lane < min(n, g0 + 64) - g0) wrow[posbase + dir * (g0 + lane)] = dacc;
+        }
+#endif
     }
 }
 
