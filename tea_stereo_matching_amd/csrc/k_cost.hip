@@ -274,8 +274,16 @@ __global__ __launch_bounds__(CW_THREADS) __attribute__((amdgpu_waves_per_eu(E ==
 #endif
     const int seg = gw % nseg;
     const int row = gw / nseg;
+    // CW_BOTH interleaves the views row by row (unit row 2y + v): view 0 and view 1 of
+    // image row y read the same two record rows (left y, right y), so both walks of a row
+    // land on one XCD and its L2 fetches those records once
+#ifdef TSM_EXP_VIEW_BLOCKS  // experiment build: view-major unit order (all of view 0 first)
     const int v = MODE == CW_BOTH ? row / H : (MODE == CW_VIEW1 ? 1 : 0);
     const int y = MODE == CW_BOTH ? row - v * H : row;
+#else
+    const int v = MODE == CW_BOTH ? (row & 1) : (MODE == CW_VIEW1 ? 1 : 0);
+    const int y = MODE == CW_BOTH ? (row >> 1) : row;
+#endif
     const int foff = v == 0 ? -P.minD : P.minD;
     const int x_lo = seg * seg_len;
     const int count0 = min(seg_len, W - x_lo);
