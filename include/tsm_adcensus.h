@@ -120,11 +120,16 @@ int tsm_adc_set_offset(tsm_adc* h, int offset);
 int tsm_adc_compute(tsm_adc* h, const uint8_t* left, const uint8_t* right, int rows, int cols,
                     size_t step, float* out, size_t out_step);
 /* Same on device-resident buffers (HBM); enqueued on `hip_stream` (NULL = the handle's
- * stream) and NOT synchronised. */
+ * stream) and NOT synchronised.  The handle's first workspace serves every call: a caller
+ * stream first waits for the workspace's earlier work, and the workspace's stream then
+ * waits for this pipeline, so calls on different streams never race on the workspace and
+ * tsm_adc_synchronize also covers work enqueued on caller streams. */
 int tsm_adc_compute_device(tsm_adc* h, const uint8_t* d_left, const uint8_t* d_right, int rows,
                            int cols, size_t step, float* d_out, size_t out_step, void* hip_stream);
 /* Batch form, the precedent being ONNXRuntimeInference::compute(vector<Mat>...) (stereo.h:381).
- * Pairs run concurrently on the handle's streams (tsm_adc_set_concurrency); synchronous. */
+ * Pairs run concurrently on the handle's streams (tsm_adc_set_concurrency); synchronous.
+ * On an error every stream is drained before returning, so no queued copy still touches
+ * the caller's buffers. */
 int tsm_adc_compute_batch(tsm_adc* h, int n, const uint8_t* const* lefts,
                           const uint8_t* const* rights, int rows, int cols, size_t step,
                           float* const* outs, size_t out_step);

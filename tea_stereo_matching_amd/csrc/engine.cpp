@@ -371,8 +371,10 @@ int validate(tsm_adc* h, const void* l, const void* r, int rows, int cols, size_
         return fail(h, TSM_ERR_UNSUPPORTED, "disparity range of " + std::to_string(L) + " labels is outside [2, " + std::to_string(kMaxLabels) + "]");
     if (h->min_disparity < 0)
         return fail(h, TSM_ERR_UNSUPPORTED, "negative minimum disparity (reference indexes its volume out of bounds, ADCensus.cpp:1398-1404)");
-    if (h->params.census_win == 0 && (h->params.lambda_hue != 1.f || h->params.lambda_saturation != 2.5f ||
-                                      h->params.lambda_intensity != 2.5f) && h->color_model == TSM_COLOR_HSI)
+    // build_luts indexes the HSI AD table by 2*hue + 5*(sat + int), exact only for the
+    // default weights (ADCensus.cpp:444-451); any census window, any other weights: refuse
+    if (h->color_model == TSM_COLOR_HSI && (h->params.lambda_hue != 1.f || h->params.lambda_saturation != 2.5f ||
+                                            h->params.lambda_intensity != 2.5f))
         return fail(h, TSM_ERR_UNSUPPORTED, "HSI AD lambdas other than (1, 2.5, 2.5)");
     return TSM_OK;
 }
@@ -566,6 +568,26 @@ int set_device(tsm_adc* h) {
     return TSM_OK;
 }
 
+// Make stream `after` wait for everything enqueued so far on stream `before`.
+int stream_after(tsm_adc* h, Workspace* w, hipStream_t before, hipStream_t after) {
+    if (before == after) return TSM_OK;
+    hipEvent_t e = take_event(w);
+    HIP_OK(hipEventRecord(e, before));
+    HIP_OK(hipStreamWaitEvent(after, e, 0));
+    w->ev_pool.push_back(e);  // reusable: the wait captured the recorded state
+    return TSM_OK;
+}
+
+// After an error in a batch, queued copies may still read/write caller buffers: drain
+// every workspace stream before handing the error back (keeps the first error message).
+int drain_after_error(tsm_adc* h, int rc) {
+    const std::string msg = h->err;
+    for (Workspace* w : h->ws)
+        if (w->stream) hipStreamSynchronize(w->stream);
+    h->err = msg;
+    return rc;
+}
+
 }  // namespace
 
 // ============================================================================
@@ -647,6 +669,9 @@ int tsm_adc_set_params(tsm_adc* h, const tsm_adc_params* in) {
     if (in->census_win != 0 && in->census_win != 1) return fail(h, TSM_ERR_ARGUMENT, "census_win must be 0 (9x7) or 1 (7x5)");
     if (in->max_length1 < 1 || in->max_length1 > 128) return fail(h, TSM_ERR_UNSUPPORTED, "max_length1 outside [1, 128]");
     if (in->voting_thresh > 20 || in->voting_thresh < 0) return fail(h, TSM_ERR_UNSUPPORTED, "voting_thresh outside [0, 20]");
+    // k_eq_blur / k_sobel are the fixed 3x3 cv::blur / cv::Canny apertures (ADCensus.cpp:1263-1264)
+    if (in->blur_kernel_size != 3) return fail(h, TSM_ERR_UNSUPPORTED, "blur_kernel_size other than 3");
+    if (in->canny_kernel_size != 3) return fail(h, TSM_ERR_UNSUPPORTED, "canny_kernel_size other than 3");
     h->params = *in;
     return TSM_OK;
 }
@@ -722,7 +747,12 @@ int tsm_adc_compute_device(tsm_adc* h, const uint8_t* dl, const uint8_t* dr, int
     Workspace* w = h->ws[0];
     if ((rc = ensure_workspace(h, w, rows, cols)) != TSM_OK) return rc;
     hipStream_t st = stream ? (hipStream_t)stream : w->stream;
-    return run_pipeline(h, w, dl, dr, step, dout, out_step, nullptr, st);
+    // The workspace buffers belong to w->stream: the caller's stream first waits for
+    // the workspace's earlier work, and w->stream then waits for this pipeline, so
+    // later calls on any stream (and tsm_adc_synchronize) are ordered after it.
+    if ((rc = stream_after(h, w, w->stream, st)) != TSM_OK) return rc;
+    if ((rc = run_pipeline(h, w, dl, dr, step, dout, out_step, nullptr, st)) != TSM_OK) return rc;
+    return stream_after(h, w, st, w->stream);
 }
 
 static int compute_host(tsm_adc* h, const uint8_t* l, const uint8_t* r, int rows, int cols,
@@ -766,13 +796,32 @@ int tsm_adc_compute_batch_device(tsm_adc* h, int n, const uint8_t* const* dls,
     const int S = h->concurrency;
     ensure_pool(h, S);
     for (int i = 0; i < n; ++i) {
-        if ((rc = validate(h, dls[i], drs[i], rows, cols, step)) != TSM_OK) return rc;
+        if ((rc = validate(h, dls[i], drs[i], rows, cols, step)) != TSM_OK) return drain_after_error(h, rc);
+        if (!douts[i] || out_step < (size_t)cols * 4)
+            return drain_after_error(h, fail(h, TSM_ERR_ARGUMENT, "output buffer"));
         Workspace* w = h->ws[i % S];
-        if ((rc = ensure_workspace(h, w, rows, cols)) != TSM_OK) return rc;
+        if ((rc = ensure_workspace(h, w, rows, cols)) != TSM_OK) return drain_after_error(h, rc);
         if ((rc = run_pipeline(h, w, dls[i], drs[i], step, douts[i], out_step, nullptr, w->stream)) != TSM_OK)
-            return rc;
+            return drain_after_error(h, rc);
     }
     return tsm_adc_synchronize(h);
+}
+
+static int enqueue_host_pair(tsm_adc* h, Workspace* w, const uint8_t* l, const uint8_t* r, int rows, int cols,
+                             size_t step, float* out, size_t out_step) {
+    int rc;
+    if ((rc = validate(h, l, r, rows, cols, step)) != TSM_OK) return rc;
+    if (!out || out_step < (size_t)cols * 4) return fail(h, TSM_ERR_ARGUMENT, "output buffer");
+    if ((rc = ensure_workspace(h, w, rows, cols)) != TSM_OK) return rc;
+    const size_t dstep = (size_t)cols * 3;
+    if ((rc = ensure_input_staging(h, w, rows, dstep, cols)) != TSM_OK) return rc;
+    HIP_OK(hipMemcpy2DAsync(w->in_left, dstep, l, step, dstep, rows, hipMemcpyHostToDevice, w->stream));
+    HIP_OK(hipMemcpy2DAsync(w->in_right, dstep, r, step, dstep, rows, hipMemcpyHostToDevice, w->stream));
+    if ((rc = run_pipeline(h, w, w->in_left, w->in_right, dstep, w->out_dev, (size_t)cols * 4, nullptr, w->stream)) != TSM_OK)
+        return rc;
+    HIP_OK(hipMemcpy2DAsync(out, out_step, w->out_dev, (size_t)cols * 4, (size_t)cols * 4, rows,
+                            hipMemcpyDeviceToHost, w->stream));
+    return TSM_OK;
 }
 
 int tsm_adc_compute_batch(tsm_adc* h, int n, const uint8_t* const* ls, const uint8_t* const* rs,
@@ -782,21 +831,11 @@ int tsm_adc_compute_batch(tsm_adc* h, int n, const uint8_t* const* ls, const uin
     if ((rc = set_device(h)) != TSM_OK) return rc;
     const int S = h->concurrency;
     ensure_pool(h, S);
-    const size_t dstep = (size_t)cols * 3;
     for (int i0 = 0; i0 < n; i0 += S) {
         const int i1 = std::min(n, i0 + S);
         for (int i = i0; i < i1; ++i) {
-            if ((rc = validate(h, ls[i], rs[i], rows, cols, step)) != TSM_OK) return rc;
-            if (!outs[i] || out_step < (size_t)cols * 4) return fail(h, TSM_ERR_ARGUMENT, "output buffer");
-            Workspace* w = h->ws[i - i0];
-            if ((rc = ensure_workspace(h, w, rows, cols)) != TSM_OK) return rc;
-            if ((rc = ensure_input_staging(h, w, rows, dstep, cols)) != TSM_OK) return rc;
-            HIP_OK(hipMemcpy2DAsync(w->in_left, dstep, ls[i], step, dstep, rows, hipMemcpyHostToDevice, w->stream));
-            HIP_OK(hipMemcpy2DAsync(w->in_right, dstep, rs[i], step, dstep, rows, hipMemcpyHostToDevice, w->stream));
-            if ((rc = run_pipeline(h, w, w->in_left, w->in_right, dstep, w->out_dev, (size_t)cols * 4, nullptr, w->stream)) != TSM_OK)
-                return rc;
-            HIP_OK(hipMemcpy2DAsync(outs[i], out_step, w->out_dev, (size_t)cols * 4, (size_t)cols * 4,
-                                    rows, hipMemcpyDeviceToHost, w->stream));
+            if ((rc = enqueue_host_pair(h, h->ws[i - i0], ls[i], rs[i], rows, cols, step, outs[i], out_step)) != TSM_OK)
+                return drain_after_error(h, rc);
         }
         if ((rc = tsm_adc_synchronize(h)) != TSM_OK) return rc;
     }
