@@ -127,7 +127,7 @@ int tsm_adc_compute(tsm_adc* h, const uint8_t* left, const uint8_t* right, int r
 int tsm_adc_compute_device(tsm_adc* h, const uint8_t* d_left, const uint8_t* d_right, int rows,
                            int cols, size_t step, float* d_out, size_t out_step, void* hip_stream);
 /* Batch form, the precedent being ONNXRuntimeInference::compute(vector<Mat>...) (stereo.h:381).
- * Pairs run concurrently on the handle's streams (tsm_adc_set_concurrency); synchronous.
+ * Pairs run in groups of tsm_adc_set_concurrency pairs (one pipeline per group); synchronous.
  * On an error every stream is drained before returning, so no queued copy still touches
  * the caller's buffers. */
 int tsm_adc_compute_batch(tsm_adc* h, int n, const uint8_t* const* lefts,
@@ -144,7 +144,9 @@ int tsm_adc_synchronize(tsm_adc* h);
 int tsm_adc_get_params(const tsm_adc* h, tsm_adc_params* out);
 int tsm_adc_set_params(tsm_adc* h, const tsm_adc_params* in);
 int tsm_adc_get_disparity_range(const tsm_adc* h, int* min_disparity, int* max_disparity);
-/* Number of concurrent pair workspaces/streams used by the batch entry points (default 2). */
+/* Pairs per group in the batch entry points (default 2, at most 16): a group of K pairs
+ * runs as one pipeline whose every launch covers the K pairs (K pair slots in one arena),
+ * and consecutive groups alternate between two streams. */
 int tsm_adc_set_concurrency(tsm_adc* h, int n_streams);
 /* 0/1 (default): serial scanline semantics.  T > 1: reproduce the deterministic
  * lock-step outcome of the reference's racy omp-static scanline schedule on T threads

@@ -2,10 +2,13 @@
 // C ABI declared in include/tsm_adcensus.h.
 //
 // A handle (tsm_adc) holds the reference's matcher state (ADCensusImpl members,
-// ADCensus.cpp:276-295) plus a pool of per-pair workspaces, each with its own HIP
-// stream and HBM buffers sized for (H, W, L).  compute() enqueues the whole pipeline
-// without any host synchronisation inside it; batch entry points round-robin pairs over
-// the workspaces so independent pairs overlap on the device.
+// ADCensus.cpp:276-295) plus up to two group workspaces, each with its own HIP stream and
+// one HBM arena of K pair slots sized for (H, W, L).  A group of K pairs runs as ONE
+// pipeline: every launch covers all K pairs (blockIdx.z = pair, slots DevParams.pstride
+// bytes apart), so the latency-bound stages (the row-serial scanline passes, the
+// refinement chain) and the launch gaps are paid once per group rather than once per
+// pair.  Batches alternate their groups between the two workspaces, so one group's tail
+// overlaps the next group's head.  No host synchronisation inside a pipeline.
 #include <hip/hip_runtime.h>
 
 #include <cmath>
@@ -85,33 +88,37 @@ struct Workspace {
     hipStream_t stream = nullptr;
     int H = 0, W = 0, L = 0, Lp = 0, model = -1, maxD = -1;
     float lambda_ad = 0, lambda_census = 0;
+    int cap = 0;          // pair slots in the arena
+    size_t slot = 0;      // bytes per pair slot (DevParams.pstride)
     size_t bytes = 0;
-    // host-API staging
+    // host-API staging: `cap` slots of in_cap bytes per input, H*W floats per output
     uint8_t* in_left = nullptr;
     uint8_t* in_right = nullptr;
     size_t in_cap = 0;
+    int in_slots = 0;
     float* out_dev = nullptr;
-    // pipeline buffers
+    // pair 0's buffers in the arena (pair p: + p * slot)
     uint32_t* img_orig = nullptr;  // [2][H][W] packed BGR
     uint32_t* img = nullptr;       // [2][H][W] matched images (== img_orig for RGB)
     uint32_t* img_tmp = nullptr;   // HSI scratch
     uint32_t* desc = nullptr;      // [2][H][W][16]
     float* vol = nullptr;          // [2][H][W][Lp]
     uint32_t* arms = nullptr;      // [2][H][W]
+    int32_t* ws = nullptr;         // [2][2][H][W] window sizes, reciprocals, descriptors
+    uint8_t* gv = nullptr;         // [2][H][gstride] (sentinel margins)
+    uint8_t* gh = nullptr;         // [2][H][gstride]
+    RefineBufs rb{};
+    // shared by the group's pairs
     uint32_t* cost_ctr = nullptr;  // cost-walk unit counter (never reset, see k_cost.hip)
     float* infvec = nullptr;       // 64 x +inf (scanline lanes past the label axis)
     uint32_t cost_ctr_base = 0;
-    int32_t* ws = nullptr;         // [2][2][H][W]
-    uint8_t* gv = nullptr;         // [2][H][gstride] (sentinel margins)
-    uint8_t* gh = nullptr;         // [2][H][gstride]
     float* lutA = nullptr;
     float* lutB = nullptr;
     int lutA_n = 0;
-    RefineBufs rb{};
     std::vector<void*> allocs;
-    // profiling
+    // profiling: per group, its stage events and pair count
     std::vector<hipEvent_t> ev_pool;
-    std::vector<std::vector<hipEvent_t>> pending;
+    std::vector<std::pair<std::vector<hipEvent_t>, int>> pending;
 };
 
 }  // namespace
@@ -160,6 +167,8 @@ void free_ws(Workspace* w) {
     w->allocs.clear();
     w->bytes = 0;
     w->H = w->W = w->L = 0;
+    w->cap = 0;
+    w->slot = 0;
 }
 
 int alloc(tsm_adc* h, Workspace* w, void** p, size_t bytes) {
@@ -171,18 +180,68 @@ int alloc(tsm_adc* h, Workspace* w, void** p, size_t bytes) {
     return TSM_OK;
 }
 
+// Per-pair slot of the arena: every buffer a pair owns, at 256-B aligned offsets.  With
+// `base` null it only measures (the offsets are what the pointers become).
+struct SlotLayout {
+    size_t off = 0;
+    char* base = nullptr;
+    template <class T>
+    void take(T*& p, size_t bytes) {
+        p = reinterpret_cast<T*>(base + off);
+        off += (bytes + 255) & ~(size_t)255;
+    }
+};
+
+void layout_slot(Workspace* w, SlotLayout& S, int H, int W, int L, int model) {
+    const size_t N = (size_t)H * W;
+    const int Lp = round_up4(L);
+    S.take(w->img_orig, 2 * N * 4);
+    if (model == TSM_COLOR_HSI) {
+        S.take(w->img, 2 * N * 4);
+        S.take(w->img_tmp, 2 * N * 4);
+    } else {
+        w->img = w->img_orig;
+        w->img_tmp = nullptr;
+    }
+    S.take(w->desc, 2 * N * 16 * 4);
+    S.take(w->vol, 2 * N * (size_t)Lp * 4);
+    S.take(w->arms, 2 * N * 4);
+    S.take(w->ws, 12 * N * 4);  // window sizes, reciprocals, packed descriptors (k_window_sizes)
+    RefineBufs& B = w->rb;
+    S.take(B.disp0, 2 * N * 4);  // [2][H][W]: the fused WTA writes view v at disp0 + v*N
+    B.disp1 = B.disp0 + N;
+    S.take(B.dm, N * 4);
+    S.take(B.dtmp, N * 4);
+    S.take(B.vote, N * 4);
+    S.take(B.samples, N * 20 * 2);
+    S.take(B.flags, N);
+    S.take(B.out_pos, N * 4);
+    S.take(B.out_list, N * 4);
+    S.take(B.hi_list, N * 4);
+    S.take(B.cvote, N * 4);
+    S.take(B.csamp, N * 20 * 2);
+    S.take(B.bsum, 2 * refine_scan_blocks((int)N) * 4 + 64);
+    S.take(B.counts, 16);
+    S.take(B.gray, N);
+    S.take(B.gray_eq, N);
+    S.take(B.hist, (256 + 64) * 4);
+    S.take(B.blurred, N);
+    S.take(B.dx, N * 2);
+    S.take(B.dy, N * 2);
+    S.take(B.mag, N * 4);
+    S.take(B.map, N);
+    S.take(B.label, N * 4);
+    S.take(B.strong, N);
+    S.take(B.edges, N);
+    S.take(B.subpix, N * 4);
+}
+
 size_t workspace_bytes(int H, int W, int L) {
-    const size_t N = (size_t)H * W, Lp = (size_t)round_up4(L);
-    size_t b = 0;
-    b += 3 * 2 * N * 4;        // img_orig, img, img_tmp
-    b += 2 * N * 16 * 4;       // desc
-    b += 2 * N * Lp * 4;       // vol
-    b += 2 * N * 4 + 256;      // arms, cost-walk counter
-    b += 12 * N * 4;           // ws, reciprocals, packed descriptors
-    b += 4 * (size_t)H * (W + 2 * grad_pad(L) + 16);  // gv, gh (upper bound)
-    b += N * (4 * 8 + 2 * 20 + 1 * 6 + 2 * 2 + 4); // refine maps
-    b += N * (4 + 2 * 20);     // carried votes / samples by outlier rank
-    return b;
+    Workspace tmp;
+    SlotLayout S;
+    layout_slot(&tmp, S, H, W, L, TSM_COLOR_HSI);
+    const size_t gs = (size_t)(((W + 2 * grad_pad(L + 255) + 15) / 16) * 16);  // gv, gh (upper bound)
+    return S.off + 2 * (2 * (size_t)H * gs + 256);
 }
 
 // Host-built exp tables: the exact float arguments the reference hands to std::exp
@@ -259,66 +318,44 @@ DevParams make_params(const tsm_adc* h, int H, int W) {
     return P;
 }
 
-int ensure_workspace(tsm_adc* h, Workspace* w, int H, int W) {
+// Workspace for groups of up to K pairs of H x W at the current range and model.
+int ensure_workspace(tsm_adc* h, Workspace* w, int H, int W, int K) {
     const int L = h->max_disparity - h->min_disparity + 1;
     if (w->stream == nullptr) HIP_OK(hipStreamCreateWithFlags(&w->stream, hipStreamNonBlocking));
     const tsm_adc_params& p = h->params;
     if (w->H == H && w->W == W && w->L == L && w->maxD == h->max_disparity && w->model == h->color_model &&
-        w->lambda_ad == p.lambda_ad && w->lambda_census == p.lambda_census)
+        w->lambda_ad == p.lambda_ad && w->lambda_census == p.lambda_census && w->cap >= K)
         return TSM_OK;
     HIP_OK(hipStreamSynchronize(w->stream));
+    const int cap = std::max(K, w->cap);
     free_ws(w);
+    if (w->in_left) { hipFree(w->in_left); w->in_left = nullptr; }
+    if (w->in_right) { hipFree(w->in_right); w->in_right = nullptr; }
+    if (w->out_dev) { hipFree(w->out_dev); w->out_dev = nullptr; }
+    w->in_cap = 0;
+    w->in_slots = 0;
     const size_t N = (size_t)H * W;
     const int Lp = round_up4(L);
     int rc;
 #define A(ptr, bytes)                                                      \
     if ((rc = alloc(h, w, (void**)&(ptr), (bytes))) != TSM_OK) { free_ws(w); return rc; }
-    A(w->img_orig, 2 * N * 4);
-    if (h->color_model == TSM_COLOR_HSI) {
-        A(w->img, 2 * N * 4);
-        A(w->img_tmp, 2 * N * 4);
-    } else {
-        w->img = w->img_orig;
-    }
-    A(w->desc, 2 * N * 16 * 4);
-    A(w->vol, 2 * N * (size_t)Lp * 4);
-    A(w->arms, 2 * N * 4);
+    // one arena of `cap` slots; pair 0's pointers are the slot offsets from its base
+    SlotLayout S;
+    layout_slot(w, S, H, W, L, h->color_model);
+    const int gp = grad_pad(h->max_disparity);
+    const size_t gs = (size_t)(((W + 2 * gp + 15) / 16) * 16);
+    S.take(w->gv, 2 * (size_t)H * gs + 64);
+    S.take(w->gh, 2 * (size_t)H * gs + 64);
+    const size_t slot = (S.off + 4095) & ~(size_t)4095;
+    char* arena = nullptr;
+    A(arena, slot * (size_t)cap);
+    S.off = 0;
+    S.base = arena;
+    layout_slot(w, S, H, W, L, h->color_model);
+    S.take(w->gv, 2 * (size_t)H * gs + 64);
+    S.take(w->gh, 2 * (size_t)H * gs + 64);
     A(w->cost_ctr, 256);
     A(w->infvec, 256);
-    A(w->ws, 12 * N * 4);  // window sizes, reciprocals, packed descriptors (k_window_sizes)
-    {
-        const int gp = grad_pad(h->max_disparity);
-        const size_t gs = (size_t)(((W + 2 * gp + 15) / 16) * 16);
-        A(w->gv, 2 * (size_t)H * gs + 64);
-        A(w->gh, 2 * (size_t)H * gs + 64);
-    }
-    RefineBufs& B = w->rb;
-    A(B.disp0, 2 * N * 4);  // [2][H][W]: the fused WTA writes view v at disp0 + v*N
-    B.disp1 = B.disp0 + N;
-    A(B.dm, N * 4);
-    A(B.dtmp, N * 4);
-    A(B.vote, N * 4);
-    A(B.samples, N * 20 * 2);
-    A(B.flags, N);
-    A(B.out_pos, N * 4);
-    A(B.out_list, N * 4);
-    A(B.hi_list, N * 4);
-    A(B.cvote, N * 4);
-    A(B.csamp, N * 20 * 2);
-    A(B.bsum, 2 * refine_scan_blocks((int)N) * 4 + 64);
-    A(B.counts, 16);
-    A(B.gray, N);
-    A(B.gray_eq, N);
-    A(B.hist, (256 + 64) * 4);
-    A(B.blurred, N);
-    A(B.dx, N * 2);
-    A(B.dy, N * 2);
-    A(B.mag, N * 4);
-    A(B.map, N);
-    A(B.label, N * 4);
-    A(B.strong, N);
-    A(B.edges, N);
-    A(B.subpix, N * 4);
     std::vector<float> la, lb;
     build_luts(p, h->color_model, la, lb);
     A(w->lutA, la.size() * 4);
@@ -327,14 +364,18 @@ int ensure_workspace(tsm_adc* h, Workspace* w, int H, int W) {
     w->lutA_n = (int)la.size();
     HIP_OK(hipMemcpy(w->lutA, la.data(), la.size() * 4, hipMemcpyHostToDevice));
     HIP_OK(hipMemcpy(w->lutB, lb.data(), lb.size() * 4, hipMemcpyHostToDevice));
-    // padded lanes of the volume are never read as labels; keep them defined anyway
-    HIP_OK(hipMemset(w->vol, 0, 2 * N * (size_t)Lp * 4));
+    // padded lanes of the volumes are never read as labels; keep the arena defined anyway
+    HIP_OK(hipMemset(arena, 0, slot * (size_t)cap));
     HIP_OK(hipMemset(w->cost_ctr, 0, 256));
     {
         std::vector<float> inf(64, std::numeric_limits<float>::infinity());
         HIP_OK(hipMemcpy(w->infvec, inf.data(), 256, hipMemcpyHostToDevice));
     }
+    (void)N;
+    (void)Lp;
     w->cost_ctr_base = 0;
+    w->cap = cap;
+    w->slot = slot;
     w->H = H;
     w->W = W;
     w->L = L;
@@ -346,17 +387,21 @@ int ensure_workspace(tsm_adc* h, Workspace* w, int H, int W) {
     return TSM_OK;
 }
 
-int ensure_input_staging(tsm_adc* h, Workspace* w, int H, size_t step, int W) {
+// Host-API staging for K pairs: K input slots of H * step bytes per view, K outputs.
+int ensure_input_staging(tsm_adc* h, Workspace* w, int H, size_t step, int W, int K) {
     const size_t need = (size_t)H * step;
-    if (w->in_cap < need) {
+    if (w->in_cap < need || w->in_slots < K) {
         if (w->in_left) { hipFree(w->in_left); w->in_left = nullptr; }
         if (w->in_right) { hipFree(w->in_right); w->in_right = nullptr; }
         if (w->out_dev) { hipFree(w->out_dev); w->out_dev = nullptr; }
-        HIP_OK(hipMalloc((void**)&w->in_left, need));
-        HIP_OK(hipMalloc((void**)&w->in_right, need));
-        w->in_cap = need;
+        const size_t cap = std::max(need, w->in_cap);
+        const int slots = std::max(K, w->in_slots);
+        HIP_OK(hipMalloc((void**)&w->in_left, cap * slots));
+        HIP_OK(hipMalloc((void**)&w->in_right, cap * slots));
+        HIP_OK(hipMalloc((void**)&w->out_dev, (size_t)H * W * 4 * slots + 256));
+        w->in_cap = cap;
+        w->in_slots = slots;
     }
-    if (w->out_dev == nullptr) HIP_OK(hipMalloc((void**)&w->out_dev, (size_t)H * W * 4 + 256));
     return TSM_OK;
 }
 
@@ -395,13 +440,17 @@ hipEvent_t take_event(Workspace* w) {
     return e;
 }
 
-// Enqueue the full pipeline for one pair on workspace w.  d_left/d_right: device BGR
-// with `step`; d_out: device fp32 with out_step.  No host synchronisation.
-int run_pipeline(tsm_adc* h, Workspace* w, const uint8_t* d_left, const uint8_t* d_right,
-                 size_t step, float* d_out, size_t out_step, const tsm_adc_dump* dump,
-                 hipStream_t st) {
+// Enqueue the full pipeline for a group of K pairs on workspace w (K <= w->cap).
+// in: device BGR images with `step`; outs: device fp32 maps with out_step.  Every launch
+// covers the K pairs.  No host synchronisation (dumps, K = 1 only, synchronise).
+int run_pipeline(tsm_adc* h, Workspace* w, int K, const PairIn& in, size_t step, const PairOut& outs,
+                 size_t out_step, const tsm_adc_dump* dump, hipStream_t st) {
     const int H = w->H, W = w->W;
-    const DevParams P = make_params(h, H, W);
+    DevParams P = make_params(h, H, W);
+    P.pstride = w->slot;
+    P.npairs = K;
+    if (K < 1 || K > w->cap || K > kMaxGroup || (dump && K != 1))
+        return fail(h, TSM_ERR_ARGUMENT, "pair group size");
     const size_t N = (size_t)H * W;
     std::vector<hipEvent_t> ev;
     auto mark = [&]() {
@@ -425,16 +474,21 @@ int run_pipeline(tsm_adc* h, Workspace* w, const uint8_t* d_left, const uint8_t*
         return TSM_OK;
     };
     int rc;
+#ifdef TSM_EXP_SKIP
+    static const int skip = [] { const char* e = getenv("TSM_SKIP"); return e ? atoi(e) : 0; }();
+#else
+    constexpr int skip = 0;
+#endif
 
     mark();
     // --- prep: pack (+HSI), census descriptors -------------------------------------
-    launch_pack(d_left, d_right, step, H, W, w->img_orig, st);
+    launch_pack(in, step, w->img_orig, P, st);
     if (h->color_model == TSM_COLOR_HSI)
-        launch_hsi(w->img_orig, w->img_tmp, w->img, H, W, (h->roi || h->mask) ? 1 : 0, st);
+        launch_hsi(w->img_orig, w->img_tmp, w->img, (h->roi || h->mask) ? 1 : 0, P, st);
     launch_census(w->img, w->desc, P, st);
     mark();
     // --- cost volume -------------------------------------------------------------
-    if (launch_cost_volume(w->img, w->desc, w->lutA, w->lutA_n, w->lutB, w->vol, P, w->cost_ctr,
+    if (!(skip & 16) && launch_cost_volume(w->img, w->desc, w->lutA, w->lutA_n, w->lutB, w->vol, P, w->cost_ctr,
                            w->cost_ctr_base, st) != 0)
         return fail(h, TSM_ERR_UNSUPPORTED, "cost volume: label count");
     mark();
@@ -481,7 +535,7 @@ int run_pipeline(tsm_adc* h, Workspace* w, const uint8_t* d_left, const uint8_t*
             const char* e = getenv("TSM_AGG_KERNEL");
             return !e ? 0 : e[0] == 'd' ? 1 : 0;
         }();
-        for (size_t i = 0; i < passes.size(); ++i) {
+        for (size_t i = 0; i < ((skip & 8) ? 0 : passes.size()); ++i) {
             const Pass& a = passes[i];
             const bool pair = i + 1 < passes.size() && a.ws && !passes[i + 1].ws &&
                               passes[i + 1].horizontal == a.horizontal;
@@ -504,10 +558,11 @@ int run_pipeline(tsm_adc* h, Workspace* w, const uint8_t* d_left, const uint8_t*
         const char* e = getenv("TSM_WTA_FUSED");
         return !(e && e[0] == '0');
     }();
-    bool ok = launch_scan_vertical(w->vol, w->gv, w->img, +1, w->infvec, P, st) == 0 &&
-              launch_scan_vertical(w->vol, w->gv, w->img, -1, w->infvec, P, st) == 0 &&
-              launch_scan_horizontal(w->vol, w->gh, w->img, +1, nullptr, 1, w->infvec, P, st) == 0;
-    if (ok && wta_fused)
+    bool ok = ((skip & 4) || (launch_scan_vertical(w->vol, w->gv, w->img, +1, w->infvec, P, st) == 0 &&
+              launch_scan_vertical(w->vol, w->gv, w->img, -1, w->infvec, P, st) == 0)) &&
+              ((skip & 2) || launch_scan_horizontal(w->vol, w->gh, w->img, +1, nullptr, 1, w->infvec, P, st) == 0);
+    if (skip & 2) {
+    } else if (ok && wta_fused)
         ok = launch_scan_horizontal(w->vol, w->gh, w->img, -1, w->rb.disp0, keep_view1 ? 1 : 0, w->infvec, P,
                                     st) == 0;
     else if (ok)
@@ -518,6 +573,7 @@ int run_pipeline(tsm_adc* h, Workspace* w, const uint8_t* d_left, const uint8_t*
     if (keep_view1 && (rc = dump_vol(dump->cost_scan, 2)) != TSM_OK) return rc;
     if (dump && dump->wta && (rc = d2h(dump->wta, w->rb.disp0, 2 * N * 4)) != TSM_OK) return rc;
     // --- refinement --------------------------------------------------------------------
+    if (skip & 1) { mark(); mark(); HIP_OK(hipGetLastError()); if (h->profiling) w->pending.emplace_back(ev, K); return TSM_OK; }
     launch_outlier(w->rb, P, st);
     if (dump && dump->outlier && (rc = d2h(dump->outlier, w->rb.dm, N * 4)) != TSM_OK) return rc;
     {
@@ -534,23 +590,24 @@ int run_pipeline(tsm_adc* h, Workspace* w, const uint8_t* d_left, const uint8_t*
     if (dump && dump->gray && (rc = d2h(dump->gray, w->rb.gray_eq, N)) != TSM_OK) return rc;
     if (dump && dump->edges && (rc = d2h(dump->edges, w->rb.edges, N)) != TSM_OK) return rc;
     if (dump && dump->adjusted && (rc = d2h(dump->adjusted, w->rb.dm, N * 4)) != TSM_OK) return rc;
-    launch_subpixel_median(w->rb, w->vol, w->img_orig, d_out, out_step, (h->roi || h->mask) ? 1 : 0,
+    launch_subpixel_median(w->rb, w->vol, w->img_orig, outs, out_step, (h->roi || h->mask) ? 1 : 0,
                            h->offset, P, st);
     if (dump && dump->subpix && (rc = d2h(dump->subpix, w->rb.subpix, N * 4)) != TSM_OK) return rc;
     mark();
     HIP_OK(hipGetLastError());
-    if (h->profiling) w->pending.push_back(ev);
+    if (h->profiling) w->pending.emplace_back(ev, K);
     return TSM_OK;
 }
 
-// Fold finished per-pair events into the handle's stage totals (call after sync).
+// Fold finished groups' events into the handle's stage totals (call after sync): a
+// group's stage span counts once per pair it carried, so ms / count is per pair.
 void collect_profile(tsm_adc* h, Workspace* w) {
-    for (auto& ev : w->pending) {
+    for (auto& [ev, K] : w->pending) {
         for (size_t k = 0; k + 1 < ev.size() && k < TSM_STAGE_COUNT; ++k) {
             float ms = 0.f;
             if (hipEventElapsedTime(&ms, ev[k], ev[k + 1]) == hipSuccess) {
                 h->stage_ms[k] += ms;
-                h->stage_cnt[k] += 1;
+                h->stage_cnt[k] += K;
             }
         }
         for (hipEvent_t e : ev) w->ev_pool.push_back(e);
@@ -617,7 +674,7 @@ int tsm_adc_destroy(tsm_adc* h) {
         if (w->in_left) hipFree(w->in_left);
         if (w->in_right) hipFree(w->in_right);
         if (w->out_dev) hipFree(w->out_dev);
-        for (auto& ev : w->pending) for (hipEvent_t e : ev) hipEventDestroy(e);
+        for (auto& pe : w->pending) for (hipEvent_t e : pe.first) hipEventDestroy(e);
         for (hipEvent_t e : w->ev_pool) hipEventDestroy(e);
         if (w->stream) hipStreamDestroy(w->stream);
         delete w;
@@ -745,14 +802,32 @@ int tsm_adc_compute_device(tsm_adc* h, const uint8_t* dl, const uint8_t* dr, int
     if ((rc = set_device(h)) != TSM_OK) return rc;
     ensure_pool(h, 1);
     Workspace* w = h->ws[0];
-    if ((rc = ensure_workspace(h, w, rows, cols)) != TSM_OK) return rc;
+    if ((rc = ensure_workspace(h, w, rows, cols, 1)) != TSM_OK) return rc;
     hipStream_t st = stream ? (hipStream_t)stream : w->stream;
     // The workspace buffers belong to w->stream: the caller's stream first waits for
     // the workspace's earlier work, and w->stream then waits for this pipeline, so
     // later calls on any stream (and tsm_adc_synchronize) are ordered after it.
     if ((rc = stream_after(h, w, w->stream, st)) != TSM_OK) return rc;
-    if ((rc = run_pipeline(h, w, dl, dr, step, dout, out_step, nullptr, st)) != TSM_OK) return rc;
+    PairIn in{};
+    PairOut out{};
+    in.left[0] = dl;
+    in.right[0] = dr;
+    out.out[0] = dout;
+    if ((rc = run_pipeline(h, w, 1, in, step, out, out_step, nullptr, st)) != TSM_OK) return rc;
     return stream_after(h, w, st, w->stream);
+}
+
+// H2D of pair i of a host batch into staging slot k of w (device step 3 * cols).
+static int stage_host_pair(tsm_adc* h, Workspace* w, int k, const uint8_t* l, const uint8_t* r, int rows,
+                           int cols, size_t step, PairIn& in) {
+    const size_t dstep = (size_t)cols * 3;
+    uint8_t* dl = w->in_left + (size_t)k * w->in_cap;
+    uint8_t* dr = w->in_right + (size_t)k * w->in_cap;
+    HIP_OK(hipMemcpy2DAsync(dl, dstep, l, step, dstep, rows, hipMemcpyHostToDevice, w->stream));
+    HIP_OK(hipMemcpy2DAsync(dr, dstep, r, step, dstep, rows, hipMemcpyHostToDevice, w->stream));
+    in.left[k] = dl;
+    in.right[k] = dr;
+    return TSM_OK;
 }
 
 static int compute_host(tsm_adc* h, const uint8_t* l, const uint8_t* r, int rows, int cols,
@@ -763,13 +838,14 @@ static int compute_host(tsm_adc* h, const uint8_t* l, const uint8_t* r, int rows
     if ((rc = set_device(h)) != TSM_OK) return rc;
     ensure_pool(h, 1);
     Workspace* w = h->ws[0];
-    if ((rc = ensure_workspace(h, w, rows, cols)) != TSM_OK) return rc;
-    if ((rc = ensure_input_staging(h, w, rows, (size_t)cols * 3, cols)) != TSM_OK) return rc;
-    const size_t dstep = (size_t)cols * 3;
-    HIP_OK(hipMemcpy2DAsync(w->in_left, dstep, l, step, dstep, rows, hipMemcpyHostToDevice, w->stream));
-    HIP_OK(hipMemcpy2DAsync(w->in_right, dstep, r, step, dstep, rows, hipMemcpyHostToDevice, w->stream));
-    if ((rc = run_pipeline(h, w, w->in_left, w->in_right, dstep, w->out_dev, (size_t)cols * 4, dump, w->stream)) != TSM_OK)
-        return rc;
+    if ((rc = ensure_workspace(h, w, rows, cols, 1)) != TSM_OK) return rc;
+    if ((rc = ensure_input_staging(h, w, rows, (size_t)cols * 3, cols, 1)) != TSM_OK) return rc;
+    PairIn in{};
+    PairOut po{};
+    if ((rc = stage_host_pair(h, w, 0, l, r, rows, cols, step, in)) != TSM_OK) return rc;
+    po.out[0] = w->out_dev;
+    if ((rc = run_pipeline(h, w, 1, in, (size_t)cols * 3, po, (size_t)cols * 4, dump, w->stream)) != TSM_OK)
+        return drain_after_error(h, rc);
     HIP_OK(hipMemcpy2DAsync(out, out_step, w->out_dev, (size_t)cols * 4, (size_t)cols * 4, rows,
                             hipMemcpyDeviceToHost, w->stream));
     HIP_OK(hipStreamSynchronize(w->stream));
@@ -787,41 +863,42 @@ int tsm_adc_compute_debug(tsm_adc* h, const uint8_t* l, const uint8_t* r, int ro
     return compute_host(h, l, r, rows, cols, step, out, out_step, dump);
 }
 
+// Batches run in groups of K = concurrency pairs, alternating between two group
+// workspaces (two streams) when there is more than one group.  K = 1 keeps one
+// workspace: pairs then run strictly one after another (per-stage timing alone).
+static int group_plan(tsm_adc* h, int n, int& K, int& nws) {
+    K = std::min(h->concurrency, kMaxGroup);
+    nws = (n > K && K > 1) ? 2 : 1;
+    return ensure_pool(h, nws);
+}
+
 int tsm_adc_compute_batch_device(tsm_adc* h, int n, const uint8_t* const* dls,
                                  const uint8_t* const* drs, int rows, int cols, size_t step,
                                  float* const* douts, size_t out_step) {
     if (!h || n < 0 || (n > 0 && (!dls || !drs || !douts))) return TSM_ERR_ARGUMENT;
     int rc;
     if ((rc = set_device(h)) != TSM_OK) return rc;
-    const int S = h->concurrency;
-    ensure_pool(h, S);
-    for (int i = 0; i < n; ++i) {
-        if ((rc = validate(h, dls[i], drs[i], rows, cols, step)) != TSM_OK) return drain_after_error(h, rc);
-        if (!douts[i] || out_step < (size_t)cols * 4)
-            return drain_after_error(h, fail(h, TSM_ERR_ARGUMENT, "output buffer"));
-        Workspace* w = h->ws[i % S];
-        if ((rc = ensure_workspace(h, w, rows, cols)) != TSM_OK) return drain_after_error(h, rc);
-        if ((rc = run_pipeline(h, w, dls[i], drs[i], step, douts[i], out_step, nullptr, w->stream)) != TSM_OK)
+    for (int i = 0; i < n; ++i) {  // everything is checked before anything is enqueued
+        if ((rc = validate(h, dls[i], drs[i], rows, cols, step)) != TSM_OK) return rc;
+        if (!douts[i] || out_step < (size_t)cols * 4) return fail(h, TSM_ERR_ARGUMENT, "output buffer");
+    }
+    int K, nws;
+    group_plan(h, n, K, nws);
+    for (int g = 0, i0 = 0; i0 < n; ++g, i0 += K) {
+        const int k = std::min(K, n - i0);
+        Workspace* w = h->ws[g % nws];
+        if ((rc = ensure_workspace(h, w, rows, cols, K)) != TSM_OK) return drain_after_error(h, rc);
+        PairIn in{};
+        PairOut out{};
+        for (int j = 0; j < k; ++j) {
+            in.left[j] = dls[i0 + j];
+            in.right[j] = drs[i0 + j];
+            out.out[j] = douts[i0 + j];
+        }
+        if ((rc = run_pipeline(h, w, k, in, step, out, out_step, nullptr, w->stream)) != TSM_OK)
             return drain_after_error(h, rc);
     }
     return tsm_adc_synchronize(h);
-}
-
-static int enqueue_host_pair(tsm_adc* h, Workspace* w, const uint8_t* l, const uint8_t* r, int rows, int cols,
-                             size_t step, float* out, size_t out_step) {
-    int rc;
-    if ((rc = validate(h, l, r, rows, cols, step)) != TSM_OK) return rc;
-    if (!out || out_step < (size_t)cols * 4) return fail(h, TSM_ERR_ARGUMENT, "output buffer");
-    if ((rc = ensure_workspace(h, w, rows, cols)) != TSM_OK) return rc;
-    const size_t dstep = (size_t)cols * 3;
-    if ((rc = ensure_input_staging(h, w, rows, dstep, cols)) != TSM_OK) return rc;
-    HIP_OK(hipMemcpy2DAsync(w->in_left, dstep, l, step, dstep, rows, hipMemcpyHostToDevice, w->stream));
-    HIP_OK(hipMemcpy2DAsync(w->in_right, dstep, r, step, dstep, rows, hipMemcpyHostToDevice, w->stream));
-    if ((rc = run_pipeline(h, w, w->in_left, w->in_right, dstep, w->out_dev, (size_t)cols * 4, nullptr, w->stream)) != TSM_OK)
-        return rc;
-    HIP_OK(hipMemcpy2DAsync(out, out_step, w->out_dev, (size_t)cols * 4, (size_t)cols * 4, rows,
-                            hipMemcpyDeviceToHost, w->stream));
-    return TSM_OK;
 }
 
 int tsm_adc_compute_batch(tsm_adc* h, int n, const uint8_t* const* ls, const uint8_t* const* rs,
@@ -829,17 +906,38 @@ int tsm_adc_compute_batch(tsm_adc* h, int n, const uint8_t* const* ls, const uin
     if (!h || n < 0 || (n > 0 && (!ls || !rs || !outs))) return TSM_ERR_ARGUMENT;
     int rc;
     if ((rc = set_device(h)) != TSM_OK) return rc;
-    const int S = h->concurrency;
-    ensure_pool(h, S);
-    for (int i0 = 0; i0 < n; i0 += S) {
-        const int i1 = std::min(n, i0 + S);
-        for (int i = i0; i < i1; ++i) {
-            if ((rc = enqueue_host_pair(h, h->ws[i - i0], ls[i], rs[i], rows, cols, step, outs[i], out_step)) != TSM_OK)
-                return drain_after_error(h, rc);
+    int K, nws;
+    group_plan(h, n, K, nws);
+    for (int g = 0, i0 = 0; i0 < n; ++g, i0 += K) {
+        const int k = std::min(K, n - i0);
+        Workspace* w = h->ws[g % nws];
+        for (int j = 0; j < k; ++j) {
+            const int i = i0 + j;
+            if ((rc = validate(h, ls[i], rs[i], rows, cols, step)) != TSM_OK) return drain_after_error(h, rc);
+            if (!outs[i] || out_step < (size_t)cols * 4)
+                return drain_after_error(h, fail(h, TSM_ERR_ARGUMENT, "output buffer"));
         }
-        if ((rc = tsm_adc_synchronize(h)) != TSM_OK) return rc;
+        if ((rc = ensure_workspace(h, w, rows, cols, K)) != TSM_OK) return drain_after_error(h, rc);
+        if ((rc = ensure_input_staging(h, w, rows, (size_t)cols * 3, cols, K)) != TSM_OK)
+            return drain_after_error(h, rc);
+        PairIn in{};
+        PairOut po{};
+        for (int j = 0; j < k; ++j) {
+            if ((rc = stage_host_pair(h, w, j, ls[i0 + j], rs[i0 + j], rows, cols, step, in)) != TSM_OK)
+                return drain_after_error(h, rc);
+            po.out[j] = w->out_dev + (size_t)j * rows * cols;
+        }
+        if ((rc = run_pipeline(h, w, k, in, (size_t)cols * 3, po, (size_t)cols * 4, nullptr, w->stream)) != TSM_OK)
+            return drain_after_error(h, rc);
+        for (int j = 0; j < k; ++j) {
+            rc = hipMemcpy2DAsync(outs[i0 + j], out_step, po.out[j], (size_t)cols * 4, (size_t)cols * 4, rows,
+                                  hipMemcpyDeviceToHost, w->stream) == hipSuccess ? TSM_OK : TSM_ERR_DEVICE;
+            if (rc != TSM_OK) return drain_after_error(h, fail(h, rc, "hipMemcpy2DAsync (output)"));
+        }
+        // a workspace's staging is reused by the group after next: that group's copies
+        // are queued behind this one's on the same stream
     }
-    return TSM_OK;
+    return tsm_adc_synchronize(h);
 }
 
 }  // extern "C"

@@ -62,8 +62,9 @@ __global__ void k_arms(const uint32_t* __restrict__ img, uint32_t* __restrict__ 
     const DevParams P = Pk;  // kernel args -> registers once (no per-use kernarg reloads)
     const int x = blockIdx.x * blockDim.x + threadIdx.x;
     const int y = blockIdx.y;
-    const int v = blockIdx.z;
+    const int v = blockIdx.z & 1;
     if (x >= P.W) return;
+    pair_shift(blockIdx.z >> 1, P.pstride, img, arms);
     const uint32_t* im = img + (size_t)v * P.H * P.W;
     uint32_t packed = 0;
     if (!(P.mask && im[(size_t)y * P.W + x] == 0)) {
@@ -89,9 +90,10 @@ __global__ void k_window_sizes(const uint32_t* __restrict__ arms, int32_t* __res
     const DevParams P = Pk;  // kernel args -> registers once (no per-use kernarg reloads)
     const int x = blockIdx.x * blockDim.x + threadIdx.x;
     const int y = blockIdx.y;
-    const int v = blockIdx.z;
+    const int v = blockIdx.z & 1;
     const int H = P.H, W = P.W;
     if (x >= W) return;
+    pair_shift(blockIdx.z >> 1, P.pstride, arms, ws);
     const uint32_t* A = arms + (size_t)v * H * W;
     const uint32_t a = A[(size_t)y * W + x];
     int hf = 0, vf = 0;
@@ -129,9 +131,10 @@ __global__ void k_color_grad(const uint32_t* __restrict__ img, uint8_t* __restri
     const DevParams P = Pk;
     const int xs = blockIdx.x * blockDim.x + threadIdx.x;
     const int y = blockIdx.y;
-    const int v = blockIdx.z;
+    const int v = blockIdx.z & 1;
     const int H = P.H, W = P.W;
     if (xs >= P.gstride) return;
+    pair_shift(blockIdx.z >> 1, P.pstride, img, gv, gh);
     const int x = xs - P.gpad;
     const uint8_t sent = (uint8_t)(P.color_diff + 1);
     const uint32_t* im = img + (size_t)v * H * W;
@@ -200,6 +203,7 @@ __global__ __launch_bounds__(AG_THREADS) void k_agg_line(float* __restrict__ vol
     const int RING = AG_SEG + 2 * A;
     const int v = blockIdx.y;
     const int line = blockIdx.x;
+    pair_shift(blockIdx.z, P.pstride, vol, arms, ws);
     const int n = horizontal ? W : H;
     const size_t es = horizontal ? (size_t)Lp : (size_t)W * Lp;  // floats between neighbours
     float* base = vol + (size_t)v * H * W * Lp + (horizontal ? (size_t)line * W * Lp : (size_t)line * Lp);
@@ -331,6 +335,7 @@ __global__ __launch_bounds__(AGD_THREADS) void k_agg_dma(float* __restrict__ vol
     const int AH = (A + AGD_SEG - 1) / AGD_SEG;     // halo chunks per side
     const int v = blockIdx.y;
     const int line = blockIdx.x;
+    pair_shift(blockIdx.z, P.pstride, vol, arms, ws);
     const int n = horizontal ? W : H;
     const size_t es = horizontal ? (size_t)Lp : (size_t)W * Lp;  // floats between neighbours
     float* base = vol + (size_t)v * H * W * Lp + (horizontal ? (size_t)line * W * Lp : (size_t)line * Lp);
@@ -585,6 +590,7 @@ constexpr int AX_MIR = 3;  // mirror slots after each ring (a 4-read block spans
 template <bool FUSED, int QT>
 __global__ __launch_bounds__(AS_THREADS) void k_agg_stream(AggStream S, DevParams Pk) {
     const DevParams P = Pk;
+    pair_shift(blockIdx.z, P.pstride, S.vol, S.arms, S.ws, S.pk, S.rcp);
     extern __shared__ __attribute__((aligned(16))) f32x4 smem_f4[];
     const int H = P.H, W = P.W, Lp = P.Lp;
     const int Q = QT > 0 ? QT : Lp >> 2;
@@ -764,6 +770,46 @@ __global__ __launch_bounds__(AS_THREADS) void k_agg_stream(AggStream S, DevParam
         return *reinterpret_cast<const f32x4*>(lp + off);  // timing experiment only
 #endif
         const uint32_t span = re - rb;
+#ifdef TSM_EXP_WIN8
+        // two blocks of 4 in flight per LDS round trip (windows of up to 8: one round trip)
+        for (; len > 4; len -= 8) {
+            const char* p = lp + off;
+            uint32_t off1 = off + 4 * Qs;
+            off1 = off1 >= re ? off1 - span : off1;
+            const char* q = lp + off1;
+            const f32x4 x0 = *reinterpret_cast<const f32x4*>(p);
+            const f32x4 x1 = *reinterpret_cast<const f32x4*>(p + Qs);
+            const f32x4 x2 = *reinterpret_cast<const f32x4*>(p + 2 * Qs);
+            const f32x4 x3 = *reinterpret_cast<const f32x4*>(p + 3 * Qs);
+            const f32x4 x4 = *reinterpret_cast<const f32x4*>(q);
+            const f32x4 x5 = *reinterpret_cast<const f32x4*>(q + Qs);
+            const f32x4 x6 = *reinterpret_cast<const f32x4*>(q + 2 * Qs);
+            const f32x4 x7 = *reinterpret_cast<const f32x4*>(q + 3 * Qs);
+            acc += x0;
+            acc += x1;
+            acc += x2;
+            acc += x3;
+            acc += x4;
+            if (len > 5) acc += x5;
+            if (len > 6) acc += x6;
+            if (len > 7) acc += x7;
+            off = off1 + 4 * Qs;
+            off = off >= re ? off - span : off;
+        }
+        if (len <= 0) return acc;
+        if (len == 4) {
+            const char* p = lp + off;
+            const f32x4 x0 = *reinterpret_cast<const f32x4*>(p);
+            const f32x4 x1 = *reinterpret_cast<const f32x4*>(p + Qs);
+            const f32x4 x2 = *reinterpret_cast<const f32x4*>(p + 2 * Qs);
+            const f32x4 x3 = *reinterpret_cast<const f32x4*>(p + 3 * Qs);
+            acc += x0;
+            acc += x1;
+            acc += x2;
+            acc += x3;
+            return acc;
+        }
+#else
         for (int nb = len >> 2; nb > 0; --nb) {
             const char* p = lp + off;
             const f32x4 x0 = *reinterpret_cast<const f32x4*>(p);
@@ -777,6 +823,7 @@ __global__ __launch_bounds__(AS_THREADS) void k_agg_stream(AggStream S, DevParam
             off += 4 * Qs;
             off = off >= re ? off - span : off;
         }
+#endif
         const int r = len & 3;
         if (r) {
             const char* p = lp + off;
@@ -896,6 +943,7 @@ static_assert(AS_AHEAD + AS_LAG <= AX_MC, "meta ring too short for the B lag");
 template <bool FUSED, int QT, bool BIG>
 __global__ __launch_bounds__(AX_THREADS) void k_agg_split(AggStream S, DevParams Pk) {
     const DevParams P = Pk;
+    pair_shift(blockIdx.z, P.pstride, S.vol, S.arms, S.ws, S.pk, S.rcp);
     extern __shared__ __attribute__((aligned(16))) f32x4 smem_f4[];
     const int H = P.H, W = P.W, Lp = P.Lp;
     const int slice = blockIdx.y;
@@ -932,7 +980,11 @@ __global__ __launch_bounds__(AX_THREADS) void k_agg_split(AggStream S, DevParams
         const int v = gl / S.nlv, line = gl - v * S.nlv;
         return (size_t)v * vstride + (size_t)line * ls;
     };
+#ifdef TSM_EXP_AGG_NOBAR
+    auto barrier = [&]() { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); };  // timing experiment only
+#else
     auto barrier = [&]() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); };
+#endif
     // sequential window sum of `len` ring pixels from LDS byte offset `off` (a slot of the
     // ring [rb, re)): whole blocks of 4 at immediate offsets (the mirror slots make every
     // block contiguous), then the 1-3 remaining pixels under uniform branches -- the
@@ -940,7 +992,50 @@ __global__ __launch_bounds__(AX_THREADS) void k_agg_split(AggStream S, DevParams
     auto window = [&](uint32_t off, int len, uint32_t rb, uint32_t re) -> f32x4 {
         f32x4 acc = f32x4{0.f, 0.f, 0.f, 0.f};
         const char* lp = lds + lane16;
+#ifdef TSM_EXP_AGG_W1
+        return *reinterpret_cast<const f32x4*>(lp + off);  // timing experiment only
+#endif
         const uint32_t span = re - rb;
+#ifdef TSM_EXP_WIN8
+        // two blocks of 4 in flight per LDS round trip (windows of up to 8: one round trip)
+        for (; len > 4; len -= 8) {
+            const char* p = lp + off;
+            uint32_t off1 = off + 4 * Qs;
+            off1 = off1 >= re ? off1 - span : off1;
+            const char* q = lp + off1;
+            const f32x4 x0 = *reinterpret_cast<const f32x4*>(p);
+            const f32x4 x1 = *reinterpret_cast<const f32x4*>(p + Qs);
+            const f32x4 x2 = *reinterpret_cast<const f32x4*>(p + 2 * Qs);
+            const f32x4 x3 = *reinterpret_cast<const f32x4*>(p + 3 * Qs);
+            const f32x4 x4 = *reinterpret_cast<const f32x4*>(q);
+            const f32x4 x5 = *reinterpret_cast<const f32x4*>(q + Qs);
+            const f32x4 x6 = *reinterpret_cast<const f32x4*>(q + 2 * Qs);
+            const f32x4 x7 = *reinterpret_cast<const f32x4*>(q + 3 * Qs);
+            acc += x0;
+            acc += x1;
+            acc += x2;
+            acc += x3;
+            acc += x4;
+            if (len > 5) acc += x5;
+            if (len > 6) acc += x6;
+            if (len > 7) acc += x7;
+            off = off1 + 4 * Qs;
+            off = off >= re ? off - span : off;
+        }
+        if (len <= 0) return acc;
+        if (len == 4) {
+            const char* p = lp + off;
+            const f32x4 x0 = *reinterpret_cast<const f32x4*>(p);
+            const f32x4 x1 = *reinterpret_cast<const f32x4*>(p + Qs);
+            const f32x4 x2 = *reinterpret_cast<const f32x4*>(p + 2 * Qs);
+            const f32x4 x3 = *reinterpret_cast<const f32x4*>(p + 3 * Qs);
+            acc += x0;
+            acc += x1;
+            acc += x2;
+            acc += x3;
+            return acc;
+        }
+#else
         for (int nb = len >> 2; nb > 0; --nb) {
             const char* p = lp + off;
             const f32x4 x0 = *reinterpret_cast<const f32x4*>(p);
@@ -954,6 +1049,7 @@ __global__ __launch_bounds__(AX_THREADS) void k_agg_split(AggStream S, DevParams
             off += 4 * Qs;
             off = off >= re ? off - span : off;
         }
+#endif
         const int r = len & 3;
         if (r) {
             const char* p = lp + off;
@@ -1001,10 +1097,14 @@ __global__ __launch_bounds__(AX_THREADS) void k_agg_split(AggStream S, DevParams
         auto issue = [&](int k) {  // chunk at (il, icc) -> slot k; past the end: re-read the last pixel
             const bool past = il >= my_lines;
             const uint32_t pos = past ? (uint32_t)(S.n - 1) : (uint32_t)min(icc * AS_SEG + w, S.n - 1);
+#ifdef TSM_EXP_AGG_NOLOAD
+            rv[k] = f32x4{(float)pos, 0.f, 0.f, 0.f};  // timing experiment only
+#else
             if (BIG)
                 rv[k] = *reinterpret_cast<const f32x4*>(ivp + (size_t)pos * es + 4 * lanec);
             else
                 rv[k] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rs_vol, voff, iv + pos * es4, 0));
+#endif
             rma[k] = (uint32_t)__builtin_amdgcn_raw_buffer_load_b32(rs_pk, vzero, ia + pos * aes4, 0);
             rmy[k] = S.ws ? (uint32_t)__builtin_amdgcn_raw_buffer_load_b32(rs_rcp, vzero, ia + pos * aes4, 0) : vzero;
             if (!past && ++icc == S.cpl) {
@@ -1118,7 +1218,11 @@ __global__ __launch_bounds__(AX_THREADS) void k_agg_split(AggStream S, DevParams
                 if (ob.cc * AS_SEG + w < S.n) {
                     const f32x4 acc = FUSED ? window(b_off, b_len, r2_off, r2_end)
                                             : *reinterpret_cast<const f32x4*>(lds + r2r + lane16);
+#ifdef TSM_EXP_AGG_NOSTORE
+                    if (vl && acc.x == -1.f) *reinterpret_cast<f32x4*>(volq + ob.off + 4 * lane) = acc;  // timing only
+#else
                     if (vl) *reinterpret_cast<f32x4*>(volq + ob.off + 4 * lane) = acc;
+#endif
                 }
                 out_step(ob);
             }
@@ -1199,7 +1303,7 @@ int launch_agg_stream(float* vol, const uint32_t* arms, const int32_t* ws, const
         const size_t slds = ((size_t)AS_RP1 + AS_RP2 + 2 * AX_MIR) * qs * 16 + (size_t)AX_MC * AS_SEG * AX_MW * 4;
         if (slds > 160 * 1024) return -1;
         (void)agg_split_lds;
-        const dim3 sgrid(G, nslice);
+        const dim3 sgrid(G, nslice, P.npairs);
         if (fused) {
             if (big) launch_split_t<true, 0, true>(S, P, sgrid, slds, st);
             else if (Q == 49) launch_split_t<true, 49, false>(S, P, sgrid, slds, st);
@@ -1219,7 +1323,7 @@ int launch_agg_stream(float* vol, const uint32_t* arms, const int32_t* ws, const
         attr_set = true;
     }
     const size_t lds = agg_stream_lds(P, fused);
-    const dim3 grid(G), block(AS_THREADS);
+    const dim3 grid(G, 1, P.npairs), block(AS_THREADS);
     if (fused) {
         if (Q == 49) hipLaunchKernelGGL((k_agg_stream<true, 49>), grid, block, lds, st, S, P);
         else hipLaunchKernelGGL((k_agg_stream<true, 0>), grid, block, lds, st, S, P);
@@ -1233,18 +1337,18 @@ int launch_agg_stream(float* vol, const uint32_t* arms, const int32_t* ws, const
 
 
 void launch_arms(const uint32_t* img, uint32_t* arms, const DevParams& P, hipStream_t st) {
-    dim3 g((P.W + 127) / 128, P.H, 2);
+    dim3 g((P.W + 127) / 128, P.H, 2 * P.npairs);
     hipLaunchKernelGGL(k_arms, g, dim3(128), 0, st, img, arms, P); trace_point("k_arms", st);
 }
 
 void launch_window_sizes(const uint32_t* arms, int32_t* ws, const DevParams& P, hipStream_t st) {
-    dim3 g((P.W + 127) / 128, P.H, 2);
+    dim3 g((P.W + 127) / 128, P.H, 2 * P.npairs);
     hipLaunchKernelGGL(k_window_sizes, g, dim3(128), 0, st, arms, ws, P); trace_point("k_window_sizes", st);
 }
 
 void launch_color_grad(const uint32_t* img, uint8_t* gv, uint8_t* gh, const DevParams& P,
                        hipStream_t st) {
-    dim3 g((P.gstride + 255) / 256, P.H, 2);
+    dim3 g((P.gstride + 255) / 256, P.H, 2 * P.npairs);
     hipLaunchKernelGGL(k_color_grad, g, dim3(256), 0, st, img, gv, gh, P); trace_point("k_color_grad", st);
 }
 
@@ -1286,7 +1390,7 @@ int launch_agg_line(float* vol, const uint32_t* arms, const int32_t* ws, int hor
                     const DevParams& P, hipStream_t st) {
     const int A = P.max_length1 - 1;
     const int J = (P.Lp / 4 + 63) / 64;
-    dim3 g(horizontal ? P.H : P.W, 2);
+    dim3 g(horizontal ? P.H : P.W, 2, P.npairs);
     static bool attr_set = false;
     if (!attr_set) {
         hipFuncSetAttribute((const void*)k_agg_line<1>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);

@@ -24,13 +24,13 @@ namespace tsm {
 // ---------------------------------------------------------------------------
 // image packing: BGR u8 (cv::Mat CV_8UC3, row step) -> u32 B | G<<8 | R<<16
 // ---------------------------------------------------------------------------
-__global__ void k_pack_bgr(const uint8_t* __restrict__ left, const uint8_t* __restrict__ right,
-                           size_t step, int H, int W, uint32_t* __restrict__ img) {
+__global__ void k_pack_bgr(PairIn in, size_t step, int H, int W, uint32_t* __restrict__ img, size_t ps) {
     const int x = blockIdx.x * blockDim.x + threadIdx.x;
     const int y = blockIdx.y;
-    const int v = blockIdx.z;
+    const int v = blockIdx.z & 1, pair = blockIdx.z >> 1;
     if (x >= W) return;
-    const uint8_t* s = (v == 0 ? left : right) + (size_t)y * step + (size_t)x * 3;
+    pair_shift(pair, ps, img);
+    const uint8_t* s = (v == 0 ? in.left[pair] : in.right[pair]) + (size_t)y * step + (size_t)x * 3;
     img[((size_t)v * H + y) * W + x] = (uint32_t)s[0] | ((uint32_t)s[1] << 8) | ((uint32_t)s[2] << 16);
 }
 
@@ -38,9 +38,10 @@ __global__ void k_pack_bgr(const uint8_t* __restrict__ left, const uint8_t* __re
 // acosf comes from the device math library, so hue bytes are not guaranteed bit-equal
 // to a given host libm (see DESIGN.md "HSI").
 __global__ void k_bgr2hsi(const uint32_t* __restrict__ src, uint32_t* __restrict__ dst, int n,
-                          int filter) {
+                          int filter, size_t ps) {
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
+    pair_shift(blockIdx.z, ps, src, dst);
     const uint32_t p = src[i];
     const float b = ch(p, 0) / 255.f, g = ch(p, 1) / 255.f, r = ch(p, 2) / 255.f;
     const float sum = b + g + r;
@@ -71,11 +72,12 @@ __global__ void k_bgr2hsi(const uint32_t* __restrict__ src, uint32_t* __restrict
 // computeGaussMedian, ADCensus.cpp:1475-1499: filter2D with the 3x3 Gaussian
 // {1,2,1}x{1,2,1}/16 (exact in fp32), BORDER_CONSTANT, saturate_cast (half-to-even).
 __global__ void k_gauss_median(const uint32_t* __restrict__ src, uint32_t* __restrict__ dst,
-                               int H, int W) {
+                               int H, int W, size_t ps) {
     const int x = blockIdx.x * blockDim.x + threadIdx.x;
     const int y = blockIdx.y;
-    const int v = blockIdx.z;
+    const int v = blockIdx.z & 1;
     if (x >= W) return;
+    pair_shift(blockIdx.z >> 1, ps, src, dst);
     const uint32_t* s = src + (size_t)v * H * W;
     int acc[3] = {0, 0, 0};
     for (int dy = -1; dy <= 1; ++dy) {
@@ -120,9 +122,10 @@ __global__ void k_census_desc(const uint32_t* __restrict__ img, uint32_t* __rest
     const DevParams P = Pk;  // kernel args -> registers once (no per-use kernarg reloads)
     const int x = blockIdx.x * blockDim.x + threadIdx.x;
     const int y = blockIdx.y;
-    const int v = blockIdx.z;
+    const int v = blockIdx.z & 1;
     const int H = P.H, W = P.W;
     if (x >= W) return;
+    pair_shift(blockIdx.z >> 1, P.pstride, img, desc);
     constexpr int hw = CW / 2, hh = CHh / 2;
     uint32_t w[12];
 #pragma unroll
@@ -247,6 +250,7 @@ __global__ __launch_bounds__(CW_THREADS) __attribute__((amdgpu_waves_per_eu(E ==
     const int lane = threadIdx.x & 63;
     (void)ctr;
     (void)ctr_base;
+    pair_shift(blockIdx.z, P.pstride, desc, vol);
     // one walk unit (view, row, segment) per wave; the unit's loads (ring prologue and
     // warm-up gather) are issued before the table fill's barrier so their latencies overlap
     // XCD-aware unit order: workgroups are dealt round-robin to the 8 XCDs, so block b runs
@@ -594,26 +598,27 @@ __global__ __launch_bounds__(CW_THREADS) __attribute__((amdgpu_waves_per_eu(E ==
 // ---------------------------------------------------------------------------
 // launchers
 // ---------------------------------------------------------------------------
-void launch_pack(const uint8_t* left, const uint8_t* right, size_t step, int H, int W,
-                 uint32_t* img, hipStream_t st) {
-    dim3 g((W + 255) / 256, H, 2);
-    hipLaunchKernelGGL(k_pack_bgr, g, dim3(256), 0, st, left, right, step, H, W, img); trace_point("k_pack_bgr", st);
+void launch_pack(const PairIn& in, size_t step, uint32_t* img, const DevParams& P, hipStream_t st) {
+    dim3 g((P.W + 255) / 256, P.H, 2 * P.npairs);
+    hipLaunchKernelGGL(k_pack_bgr, g, dim3(256), 0, st, in, step, P.H, P.W, img, P.pstride); trace_point("k_pack_bgr", st);
 }
 
-void launch_hsi(const uint32_t* src, uint32_t* tmp, uint32_t* dst, int H, int W, int filter,
+void launch_hsi(const uint32_t* src, uint32_t* tmp, uint32_t* dst, int filter, const DevParams& P,
                 hipStream_t st) {
+    const int H = P.H, W = P.W;
     const int n = 2 * H * W;
+    const dim3 g1((n + 255) / 256, 1, P.npairs);
     if (filter) {
-        hipLaunchKernelGGL(k_bgr2hsi, dim3((n + 255) / 256), dim3(256), 0, st, src, dst, n, 1); trace_point("k_bgr2hsi", st);
+        hipLaunchKernelGGL(k_bgr2hsi, g1, dim3(256), 0, st, src, dst, n, 1, P.pstride); trace_point("k_bgr2hsi", st);
     } else {
-        hipLaunchKernelGGL(k_bgr2hsi, dim3((n + 255) / 256), dim3(256), 0, st, src, tmp, n, 0); trace_point("k_bgr2hsi", st);
-        dim3 g((W + 255) / 256, H, 2);
-        hipLaunchKernelGGL(k_gauss_median, g, dim3(256), 0, st, tmp, dst, H, W); trace_point("k_gauss_median", st);
+        hipLaunchKernelGGL(k_bgr2hsi, g1, dim3(256), 0, st, src, tmp, n, 0, P.pstride); trace_point("k_bgr2hsi", st);
+        dim3 g((W + 255) / 256, H, 2 * P.npairs);
+        hipLaunchKernelGGL(k_gauss_median, g, dim3(256), 0, st, tmp, dst, H, W, P.pstride); trace_point("k_gauss_median", st);
     }
 }
 
 void launch_census(const uint32_t* img, uint32_t* desc, const DevParams& P, hipStream_t st) {
-    dim3 g((P.W + 127) / 128, P.H, 2);
+    dim3 g((P.W + 127) / 128, P.H, 2 * P.npairs);
     const bool hsi = P.color_model == 1;
     if (P.censusW == 7) {
         if (hsi) hipLaunchKernelGGL((k_census_desc<7, 5, true>), g, dim3(128), 0, st, img, desc, P);
@@ -656,6 +661,7 @@ __global__ void k_shear_tail(float* __restrict__ vol, DevParams Pk) {
     if (i >= span * Q) return;
     const int x1 = P.W - span + i / Q, l = i % Q;
     if (x1 + 4 * l <= P.W) return;
+    pair_shift(blockIdx.z, P.pstride, vol);
     const float inf = __int_as_float(0x7f800000);
     f32x4 o;
     o.x = 4 * l + 0 < P.L ? 2.f : inf;
@@ -674,14 +680,16 @@ static void launch_cost_t(const uint32_t* desc, const float* lutA, int lutA_n, c
     const int units = (MODE == CW_BOTH ? 2 : 1) * P.H * nseg;
     const int waves = units;
     const int wpb = CW_THREADS / 64;
-    dim3 g((waves + wpb - 1) / wpb);
+    // whole multiples of the 8 XCDs per pair, so every pair's blocks keep the same
+    // block -> XCD dealing (the unit remap in the kernel relies on it)
+    dim3 g(((waves + wpb - 1) / wpb + 7) / 8 * 8, 1, P.npairs);
     hipLaunchKernelGGL((k_cost_walk<E, HSI, MASK, MODE>), g, dim3(CW_THREADS), cost_volume_lds_bytes(P, lutA_n),
                        st, desc, lutA, lutA_n, lutB, vol, P, seg_len, nseg, ctr, ctr_base);
     trace_point("k_cost_walk", st);
     if (MODE == CW_SHEAR) {
         const int Q = P.Lp >> 2;
         const int n = (P.W < 4 * Q ? P.W : 4 * Q) * Q;
-        hipLaunchKernelGGL(k_shear_tail, dim3((n + 255) / 256, P.H), dim3(256), 0, st, vol, P);
+        hipLaunchKernelGGL(k_shear_tail, dim3((n + 255) / 256, P.H, P.npairs), dim3(256), 0, st, vol, P);
         trace_point("k_shear_tail", st);
     }
     ctr_base += (uint32_t)units + (uint32_t)(g.x * wpb);  // every wave overshoots once

@@ -14,6 +14,7 @@
 //                                    (OpenCV 4.x semantics) -> edge-pixel adjustment;
 //                                    Canny hysteresis as lock-free union-find
 //   subpixelEnhancement :1344-1374   parabola fit + medianBlur 3x3 (fp32, replicate)
+#include <algorithm>
 #include <utility>
 
 #include "tsm_device.h"
@@ -25,7 +26,8 @@ constexpr int kMaxSamples = 20; // = votingThresh: a low-vote outlier holds <= 2
 
 // zero-fill on the stream by a kernel (keeps every producer/consumer inside the
 // kernel-ordering domain; no DMA-engine writes between kernels)
-__global__ void k_zero_u32(uint32_t* __restrict__ p, int n) {
+__global__ void k_zero_u32(uint32_t* __restrict__ p, int n, size_t ps) {
+    pair_shift(blockIdx.z, ps, p);
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i < n) p[i] = 0u;
 }
@@ -36,6 +38,7 @@ __global__ void k_zero_u32(uint32_t* __restrict__ p, int n) {
 __global__ void k_outlier(const int32_t* __restrict__ dl, const int32_t* __restrict__ dr,
                           int32_t* __restrict__ out, DevParams Pk) {
     const DevParams P = Pk;  // kernel args -> registers once (no per-use kernarg reloads)
+    pair_shift(blockIdx.z, P.pstride, dl, dr, out);
     const int x = blockIdx.x * blockDim.x + threadIdx.x;
     const int y = blockIdx.y;
     const int W = P.W;
@@ -58,6 +61,7 @@ __global__ void k_outlier(const int32_t* __restrict__ dl, const int32_t* __restr
 __global__ __launch_bounds__(256) void k_outlier_row(const int32_t* __restrict__ dl, const int32_t* __restrict__ dr,
                                                      int32_t* __restrict__ out, DevParams Pk) {
     const DevParams P = Pk;
+    pair_shift(blockIdx.z, P.pstride, dl, dr, out);
     extern __shared__ uint8_t hit[];
     const int y = blockIdx.x;
     const int W = P.W;
@@ -92,6 +96,7 @@ __global__ void k_vote_count(const int32_t* __restrict__ disp, int32_t* __restri
                              int32_t* __restrict__ vote, uint16_t* __restrict__ samples,
                              uint8_t* __restrict__ flags, int hf, DevParams Pk) {
     const DevParams P = Pk;  // kernel args -> registers once (no per-use kernarg reloads)
+    pair_shift(blockIdx.z, P.pstride, disp, dtmp, arms, vote, samples, flags);
     const int x = blockIdx.x * blockDim.x + threadIdx.x;
     const int y = blockIdx.y;
     const int W = P.W;
@@ -134,6 +139,7 @@ __global__ __launch_bounds__(256) void k_vote_count_par(const int32_t* __restric
                                                         uint16_t* __restrict__ samples,
                                                         uint8_t* __restrict__ flags, int hf, DevParams Pk) {
     const DevParams P = Pk;
+    pair_shift(blockIdx.z, P.pstride, disp, dtmp, arms, vote, samples, flags);
     const int lane = threadIdx.x & 63, sub = lane & 15, base = lane & ~15;
     const int x = (blockIdx.x * blockDim.x + threadIdx.x) >> 4;
     const int y = blockIdx.y;
@@ -208,7 +214,8 @@ __device__ __forceinline__ void block_scan2(int& a, int& b, int* sa, int* sb) {
     b = ib - b;
 }
 
-__global__ void k_scan_count(const uint8_t* __restrict__ flags, int n, int32_t* __restrict__ bsum) {
+__global__ void k_scan_count(const uint8_t* __restrict__ flags, int n, int32_t* __restrict__ bsum, size_t ps) {
+    pair_shift(blockIdx.z, ps, flags, bsum);
     __shared__ int sa[SC_THREADS], sb[SC_THREADS];
     const int base = blockIdx.x * SC_BLOCK + threadIdx.x * SC_ITEMS;
     int a = 0, b = 0;
@@ -223,7 +230,8 @@ __global__ void k_scan_count(const uint8_t* __restrict__ flags, int n, int32_t* 
     }
 }
 
-__global__ void k_scan_blocks(int32_t* __restrict__ bsum, int nb, int32_t* __restrict__ counts) {
+__global__ void k_scan_blocks(int32_t* __restrict__ bsum, int nb, int32_t* __restrict__ counts, size_t ps) {
+    pair_shift(blockIdx.z, ps, bsum, counts);
     // single block: exclusive scan of nb block totals (nb <= 1024 * 8)
     __shared__ int sa[SC_THREADS], sb[SC_THREADS];
     const int per = (nb + SC_THREADS - 1) / SC_THREADS;
@@ -246,7 +254,8 @@ __global__ void k_scan_blocks(int32_t* __restrict__ bsum, int nb, int32_t* __res
 
 __global__ void k_scan_scatter(const uint8_t* __restrict__ flags, int n,
                                const int32_t* __restrict__ bsum, int32_t* __restrict__ out_pos,
-                               int32_t* __restrict__ out_list, int32_t* __restrict__ hi_list) {
+                               int32_t* __restrict__ out_list, int32_t* __restrict__ hi_list, size_t ps) {
+    pair_shift(blockIdx.z, ps, flags, bsum, out_pos, out_list, hi_list);
     __shared__ int sa[SC_THREADS], sb[SC_THREADS];
     const int base = blockIdx.x * SC_BLOCK + threadIdx.x * SC_ITEMS;
     int a = 0, b = 0;
@@ -271,7 +280,8 @@ __global__ void k_scan_scatter(const uint8_t* __restrict__ flags, int n,
 // 40-B sample record moved as ten dwords).
 __global__ void k_rank_samples(const int32_t* __restrict__ out_list, const int32_t* __restrict__ counts,
                                const int32_t* __restrict__ vote, const uint16_t* __restrict__ samples,
-                               int32_t* __restrict__ cvote, uint16_t* __restrict__ csamp) {
+                               int32_t* __restrict__ cvote, uint16_t* __restrict__ csamp, size_t ps) {
+    pair_shift(blockIdx.z, ps, out_list, counts, vote, samples, cvote, csamp);
     const int a = blockIdx.x * blockDim.x + threadIdx.x;
     if (a >= counts[0]) return;
     const int p = out_list[a];
@@ -295,6 +305,7 @@ __global__ __launch_bounds__(VD_THREADS) void k_vote_decide(
     const uint16_t* __restrict__ csamp,
     const int32_t* __restrict__ hi_list, const int32_t* __restrict__ counts, int hf, DevParams Pk) {
     const DevParams P = Pk;  // kernel args -> registers once (no per-use kernarg reloads)
+    pair_shift(blockIdx.z, P.pstride, disp, dtmp, arms, vote, samples, out_pos, cvote, csamp, hi_list, counts);
     extern __shared__ int hist_all[];
     const int L = P.L, W = P.W, minD = P.minD;
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
@@ -376,6 +387,7 @@ __constant__ int c_ray_w[16] = {0, 2, 2, 2, 0, -2, -2, -2, 1, 2, 2, 1, -1, -2, -
 __global__ void k_interp(const int32_t* __restrict__ disp, int32_t* __restrict__ out,
                          const uint32_t* __restrict__ img0, DevParams Pk) {
     const DevParams P = Pk;  // kernel args -> registers once (no per-use kernarg reloads)
+    pair_shift(blockIdx.z, P.pstride, disp, out, img0);
     const int x = blockIdx.x * blockDim.x + threadIdx.x;
     const int y = blockIdx.y;
     const int H = P.H, W = P.W, minD = P.minD;
@@ -423,6 +435,7 @@ __global__ void k_interp(const int32_t* __restrict__ disp, int32_t* __restrict__
 __global__ __launch_bounds__(256) void k_interp_rays(const int32_t* __restrict__ disp, int32_t* __restrict__ out,
                                                      const uint32_t* __restrict__ img0, DevParams Pk) {
     const DevParams P = Pk;
+    pair_shift(blockIdx.z, P.pstride, disp, out, img0);
     const int lane = threadIdx.x & 63;
     const int dir = lane & 15;
     const int x = (blockIdx.x * blockDim.x + threadIdx.x) >> 4;  // 16 lanes per pixel
@@ -480,7 +493,8 @@ __global__ __launch_bounds__(256) void k_interp_rays(const int32_t* __restrict__
 // discontinuity adjustment: gray -> equalizeHist -> blur -> Canny -> adjust
 // ---------------------------------------------------------------------------
 __global__ void k_gray_hist(const int32_t* __restrict__ disp, uint8_t* __restrict__ gray,
-                            int32_t* __restrict__ hist, int n) {
+                            int32_t* __restrict__ hist, int n, size_t ps) {
+    pair_shift(blockIdx.z, ps, disp, gray, hist);
     __shared__ int h[256];
     h[threadIdx.x] = 0;
     __syncthreads();
@@ -503,7 +517,8 @@ __device__ __forceinline__ int reflect101(int i, int n) {
 
 // equalizeHist LUT (imgproc histogram.cpp): lut[i] = saturate_cast<uchar>(sum * scale),
 // scale = 255.f / (total - hist[first nonzero]); one wave, serial 256-entry prefix.
-__global__ void k_eq_lut(const int32_t* __restrict__ hist, uint8_t* __restrict__ lut_out, int total) {
+__global__ void k_eq_lut(const int32_t* __restrict__ hist, uint8_t* __restrict__ lut_out, int total, size_t ps) {
+    pair_shift(blockIdx.z, ps, hist, lut_out);
     if (threadIdx.x != 0) return;
     uint8_t* lut = lut_out;
     int i = 0;
@@ -527,7 +542,8 @@ __global__ void k_eq_lut(const int32_t* __restrict__ hist, uint8_t* __restrict__
 // blur 3x3 BORDER_REFLECT_101 of the equalised map with the ColumnSum<ushort,uchar>
 // fixed-point divide ((s+4)*932068)>>23 == round(s/9).
 __global__ void k_eq_blur(const uint8_t* __restrict__ gray, const uint8_t* __restrict__ lut_g,
-                          uint8_t* __restrict__ eq_out, uint8_t* __restrict__ blurred, int H, int W) {
+                          uint8_t* __restrict__ eq_out, uint8_t* __restrict__ blurred, int H, int W, size_t ps) {
+    pair_shift(blockIdx.z, ps, gray, lut_g, eq_out, blurred);
     __shared__ uint8_t lut[256];
     lut[threadIdx.x] = lut_g[threadIdx.x];
     __syncthreads();
@@ -545,7 +561,8 @@ __global__ void k_eq_blur(const uint8_t* __restrict__ gray, const uint8_t* __res
 
 // Sobel 3x3 (BORDER_REPLICATE) -> dx, dy (CV_16S), L1 magnitude.
 __global__ void k_sobel(const uint8_t* __restrict__ src, int16_t* __restrict__ dx,
-                        int16_t* __restrict__ dy, int32_t* __restrict__ mag, int H, int W) {
+                        int16_t* __restrict__ dy, int32_t* __restrict__ mag, int H, int W, size_t ps) {
+    pair_shift(blockIdx.z, ps, src, dx, dy, mag);
     const int x = blockIdx.x * blockDim.x + threadIdx.x;
     const int y = blockIdx.y;
     if (x >= W) return;
@@ -568,7 +585,8 @@ __global__ void k_sobel(const uint8_t* __restrict__ src, int16_t* __restrict__ d
 // map: 1 = not an edge, 0 = weak candidate, 2 = strong (m > high).
 __global__ void k_nms(const int16_t* __restrict__ dx, const int16_t* __restrict__ dy,
                       const int32_t* __restrict__ mag, uint8_t* __restrict__ map, int H, int W,
-                      int low, int high) {
+                      int low, int high, size_t ps) {
+    pair_shift(blockIdx.z, ps, dx, dy, mag, map);
     const int x = blockIdx.x * blockDim.x + threadIdx.x;
     const int y = blockIdx.y;
     if (x >= W) return;
@@ -622,12 +640,14 @@ __device__ __forceinline__ void uf_union(int* parent, int a, int b) {
     }
 }
 
-__global__ void k_uf_init(const uint8_t* __restrict__ map, int32_t* __restrict__ label, int n) {
+__global__ void k_uf_init(const uint8_t* __restrict__ map, int32_t* __restrict__ label, int n, size_t ps) {
+    pair_shift(blockIdx.z, ps, map, label);
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i < n) label[i] = map[i] != 1 ? i : -1;
 }
 
-__global__ void k_uf_merge(const uint8_t* __restrict__ map, int32_t* __restrict__ label, int H, int W) {
+__global__ void k_uf_merge(const uint8_t* __restrict__ map, int32_t* __restrict__ label, int H, int W, size_t ps) {
+    pair_shift(blockIdx.z, ps, map, label);
     const int x = blockIdx.x * blockDim.x + threadIdx.x;
     const int y = blockIdx.y;
     if (x >= W) return;
@@ -668,7 +688,8 @@ __device__ __forceinline__ void lds_union(int* lab, int a, int b) {
 }
 
 __global__ __launch_bounds__(256) void k_uf_tile(const uint8_t* __restrict__ map, int32_t* __restrict__ label,
-                                                 int H, int W) {
+                                                 int H, int W, size_t ps) {
+    pair_shift(blockIdx.z, ps, map, label);
     __shared__ int lab[UT * UT];
     const int tx0 = blockIdx.x * UT, ty0 = blockIdx.y * UT;
     for (int k = threadIdx.x; k < UT * UT; k += 256) {
@@ -699,7 +720,8 @@ __global__ __launch_bounds__(256) void k_uf_tile(const uint8_t* __restrict__ map
     }
 }
 
-__global__ void k_uf_edges(const uint8_t* __restrict__ map, int32_t* __restrict__ label, int H, int W) {
+__global__ void k_uf_edges(const uint8_t* __restrict__ map, int32_t* __restrict__ label, int H, int W, size_t ps) {
+    pair_shift(blockIdx.z, ps, map, label);
     const int x = blockIdx.x * blockDim.x + threadIdx.x;
     const int y = blockIdx.y;
     if (x >= W) return;
@@ -716,7 +738,8 @@ __global__ void k_uf_edges(const uint8_t* __restrict__ map, int32_t* __restrict_
 }
 
 __global__ void k_uf_flatten_mark(const uint8_t* __restrict__ map, int32_t* __restrict__ label,
-                                  uint8_t* __restrict__ strong, int n) {
+                                  uint8_t* __restrict__ strong, int n, size_t ps) {
+    pair_shift(blockIdx.z, ps, map, label, strong);
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n || map[i] == 1) return;
     int r = i;
@@ -726,7 +749,8 @@ __global__ void k_uf_flatten_mark(const uint8_t* __restrict__ map, int32_t* __re
 }
 
 __global__ void k_uf_final(const uint8_t* __restrict__ map, const int32_t* __restrict__ label,
-                           const uint8_t* __restrict__ strong, uint8_t* __restrict__ edges, int n) {
+                           const uint8_t* __restrict__ strong, uint8_t* __restrict__ edges, int n, size_t ps) {
+    pair_shift(blockIdx.z, ps, map, label, strong, edges);
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
     edges[i] = (map[i] != 1 && strong[label[i]]) ? 255 : 0;
@@ -737,6 +761,7 @@ __global__ void k_adjust(const int32_t* __restrict__ disp, int32_t* __restrict__
                          const uint8_t* __restrict__ edges, const float* __restrict__ vol0,
                          DevParams Pk) {
     const DevParams P = Pk;  // kernel args -> registers once (no per-use kernarg reloads)
+    pair_shift(blockIdx.z, P.pstride, disp, out, edges, vol0);
     const int x = blockIdx.x * blockDim.x + threadIdx.x;
     const int y = blockIdx.y;
     const int H = P.H, W = P.W, minD = P.minD, Lp = P.Lp;
@@ -781,6 +806,7 @@ __global__ void k_adjust(const int32_t* __restrict__ disp, int32_t* __restrict__
 __global__ void k_subpix(const int32_t* __restrict__ disp, const float* __restrict__ vol0,
                          float* __restrict__ sub, DevParams Pk) {
     const DevParams P = Pk;  // kernel args -> registers once (no per-use kernarg reloads)
+    pair_shift(blockIdx.z, P.pstride, disp, vol0, sub);
     const int x = blockIdx.x * blockDim.x + threadIdx.x;
     const int y = blockIdx.y;
     const int W = P.W, minD = P.minD, Lp = P.Lp;
@@ -804,9 +830,11 @@ __device__ __forceinline__ void sort2(float& a, float& b) {
 }
 
 // medianBlur 3x3 CV_32F (BORDER_REPLICATE) + ROI/mask post-processing (:388-403) + store.
-__global__ void k_median_out(const float* __restrict__ sub, float* __restrict__ out,
+__global__ void k_median_out(const float* __restrict__ sub, PairOut outs,
                              size_t out_step, const uint32_t* __restrict__ orig_left,
-                             int roi_or_mask, int offset, int H, int W) {
+                             int roi_or_mask, int offset, int H, int W, size_t ps) {
+    float* out = outs.out[blockIdx.z];
+    pair_shift(blockIdx.z, ps, sub, orig_left);
     const int x = blockIdx.x * blockDim.x + threadIdx.x;
     const int y = blockIdx.y;
     if (x >= W) return;
@@ -857,7 +885,9 @@ __global__ void k_arms_to_ref(const uint32_t* __restrict__ arms, int32_t* __rest
 // ---------------------------------------------------------------------------
 size_t refine_scan_blocks(int n) { return (size_t)(n + SC_BLOCK - 1) / SC_BLOCK; }
 
-static dim3 grid2d(int W, int H, int bx) { return dim3((W + bx - 1) / bx, H); }
+// every refinement launch covers the group's P.npairs pairs (blockIdx.z = pair)
+static dim3 grid2d(int W, int H, int bx, const DevParams& P) { return dim3((W + bx - 1) / bx, H, P.npairs); }
+static dim3 grid1d(size_t n, const DevParams& P) { return dim3((unsigned)n, 1, P.npairs); }
 
 void launch_outlier(RefineBufs& B, const DevParams& P, hipStream_t st) {
     static const bool serial = [] {
@@ -865,9 +895,9 @@ void launch_outlier(RefineBufs& B, const DevParams& P, hipStream_t st) {
         return e && e[0] == '1';
     }();
     if (serial)
-        hipLaunchKernelGGL(k_outlier, grid2d(P.W, P.H, 256), dim3(256), 0, st, B.disp0, B.disp1, B.dm, P);
+        hipLaunchKernelGGL(k_outlier, grid2d(P.W, P.H, 256, P), dim3(256), 0, st, B.disp0, B.disp1, B.dm, P);
     else
-        hipLaunchKernelGGL(k_outlier_row, dim3(P.H), dim3(256), (size_t)P.W, st, B.disp0, B.disp1, B.dm, P);
+        hipLaunchKernelGGL(k_outlier_row, grid1d(P.H, P), dim3(256), (size_t)P.W, st, B.disp0, B.disp1, B.dm, P);
     trace_point("k_outlier", st);
 }
 
@@ -876,25 +906,28 @@ void launch_region_voting(RefineBufs& B, const uint32_t* arms0, int hf, const De
                           hipStream_t st) {
     const int n = P.H * P.W;
     const int nb = (int)refine_scan_blocks(n);
+    const size_t ps = P.pstride;
     static const bool serial = [] {
         const char* e = getenv("TSM_VOTE_SERIAL");  // A/B: the one-thread-per-pixel count
         return e && e[0] == '1';
     }();
     if (serial)
-        hipLaunchKernelGGL(k_vote_count, grid2d(P.W, P.H, 128), dim3(128), 0, st, B.dm, B.dtmp, arms0,
+        hipLaunchKernelGGL(k_vote_count, grid2d(P.W, P.H, 128, P), dim3(128), 0, st, B.dm, B.dtmp, arms0,
                            B.vote, B.samples, B.flags, hf, P);
     else
-        hipLaunchKernelGGL(k_vote_count_par, grid2d(P.W * 16, P.H, 256), dim3(256), 0, st, B.dm, B.dtmp,
+        hipLaunchKernelGGL(k_vote_count_par, grid2d(P.W * 16, P.H, 256, P), dim3(256), 0, st, B.dm, B.dtmp,
                            arms0, B.vote, B.samples, B.flags, hf, P);
     trace_point("k_vote_count", st);
-    hipLaunchKernelGGL(k_scan_count, dim3(nb), dim3(SC_THREADS), 0, st, B.flags, n, B.bsum); trace_point("k_scan_count", st);
-    hipLaunchKernelGGL(k_scan_blocks, dim3(1), dim3(SC_THREADS), 0, st, B.bsum, nb, B.counts); trace_point("k_scan_blocks", st);
-    hipLaunchKernelGGL(k_scan_scatter, dim3(nb), dim3(SC_THREADS), 0, st, B.flags, n, B.bsum,
-                       B.out_pos, B.out_list, B.hi_list); trace_point("k_scan_scatter", st);
-    hipLaunchKernelGGL(k_rank_samples, dim3((n + 255) / 256), dim3(256), 0, st, B.out_list, B.counts, B.vote,
-                       B.samples, B.cvote, B.csamp); trace_point("k_rank_samples", st);
+    hipLaunchKernelGGL(k_scan_count, grid1d(nb, P), dim3(SC_THREADS), 0, st, B.flags, n, B.bsum, ps); trace_point("k_scan_count", st);
+    hipLaunchKernelGGL(k_scan_blocks, grid1d(1, P), dim3(SC_THREADS), 0, st, B.bsum, nb, B.counts, ps); trace_point("k_scan_blocks", st);
+    hipLaunchKernelGGL(k_scan_scatter, grid1d(nb, P), dim3(SC_THREADS), 0, st, B.flags, n, B.bsum,
+                       B.out_pos, B.out_list, B.hi_list, ps); trace_point("k_scan_scatter", st);
+    hipLaunchKernelGGL(k_rank_samples, grid1d((n + 255) / 256, P), dim3(256), 0, st, B.out_list, B.counts, B.vote,
+                       B.samples, B.cvote, B.csamp, ps); trace_point("k_rank_samples", st);
     const size_t lds = (size_t)(VD_THREADS / 64) * P.L * sizeof(int);
-    hipLaunchKernelGGL(k_vote_decide, dim3(1024), dim3(VD_THREADS), lds, st, B.dm, B.dtmp, arms0,
+    // one wave per high-vote outlier (grid-stride); ~4096 waves over the whole group
+    const int vd_blocks = std::max(128, 1024 / std::max(1, P.npairs));
+    hipLaunchKernelGGL(k_vote_decide, grid1d(vd_blocks, P), dim3(VD_THREADS), lds, st, B.dm, B.dtmp, arms0,
                        B.vote, B.samples, B.out_pos, B.cvote, B.csamp, B.hi_list, B.counts, hf, P); trace_point("k_vote_decide", st);
     std::swap(B.dm, B.dtmp);
 }
@@ -906,9 +939,9 @@ void launch_interpolation(RefineBufs& B, const uint32_t* img0, const DevParams& 
         return e && e[0] == '1';
     }();
     if (serial)
-        hipLaunchKernelGGL(k_interp, grid2d(P.W, P.H, 128), dim3(128), 0, st, B.dm, B.dtmp, img0, P);
+        hipLaunchKernelGGL(k_interp, grid2d(P.W, P.H, 128, P), dim3(128), 0, st, B.dm, B.dtmp, img0, P);
     else
-        hipLaunchKernelGGL(k_interp_rays, grid2d(P.W * 16, P.H, 256), dim3(256), 0, st, B.dm, B.dtmp, img0, P);
+        hipLaunchKernelGGL(k_interp_rays, grid2d(P.W * 16, P.H, 256, P), dim3(256), 0, st, B.dm, B.dtmp, img0, P);
     trace_point("k_interp", st);
     std::swap(B.dm, B.dtmp);
 }
@@ -916,40 +949,41 @@ void launch_interpolation(RefineBufs& B, const uint32_t* img0, const DevParams& 
 void launch_discontinuity(RefineBufs& B, const float* vol0, const DevParams& P,
                           hipStream_t st) {
     const int n = P.H * P.W;
-    hipLaunchKernelGGL(k_zero_u32, dim3(1), dim3(256), 0, st, reinterpret_cast<uint32_t*>(B.hist), 256); trace_point("k_zero_u32", st);
-    hipLaunchKernelGGL(k_gray_hist, dim3(min((n + 255) / 256, 1024)), dim3(256), 0, st, B.dm, B.gray, B.hist, n); trace_point("k_gray_hist", st);
+    const size_t ps = P.pstride;
+    hipLaunchKernelGGL(k_zero_u32, grid1d(1, P), dim3(256), 0, st, reinterpret_cast<uint32_t*>(B.hist), 256, ps); trace_point("k_zero_u32", st);
+    hipLaunchKernelGGL(k_gray_hist, grid1d(std::min((n + 255) / 256, 1024), P), dim3(256), 0, st, B.dm, B.gray, B.hist, n, ps); trace_point("k_gray_hist", st);
     uint8_t* lut = reinterpret_cast<uint8_t*>(B.hist + 256);
-    hipLaunchKernelGGL(k_eq_lut, dim3(1), dim3(64), 0, st, B.hist, lut, n); trace_point("k_eq_lut", st);
-    hipLaunchKernelGGL(k_eq_blur, grid2d(P.W, P.H, 256), dim3(256), 0, st, B.gray, lut,
-                       B.gray_eq, B.blurred, P.H, P.W); trace_point("k_eq_blur", st);
-    hipLaunchKernelGGL(k_sobel, grid2d(P.W, P.H, 256), dim3(256), 0, st, B.blurred, B.dx, B.dy, B.mag, P.H, P.W); trace_point("k_sobel", st);
-    hipLaunchKernelGGL(k_nms, grid2d(P.W, P.H, 256), dim3(256), 0, st, B.dx, B.dy, B.mag, B.map,
-                       P.H, P.W, P.canny_low, P.canny_high); trace_point("k_nms", st);
+    hipLaunchKernelGGL(k_eq_lut, grid1d(1, P), dim3(64), 0, st, B.hist, lut, n, ps); trace_point("k_eq_lut", st);
+    hipLaunchKernelGGL(k_eq_blur, grid2d(P.W, P.H, 256, P), dim3(256), 0, st, B.gray, lut,
+                       B.gray_eq, B.blurred, P.H, P.W, ps); trace_point("k_eq_blur", st);
+    hipLaunchKernelGGL(k_sobel, grid2d(P.W, P.H, 256, P), dim3(256), 0, st, B.blurred, B.dx, B.dy, B.mag, P.H, P.W, ps); trace_point("k_sobel", st);
+    hipLaunchKernelGGL(k_nms, grid2d(P.W, P.H, 256, P), dim3(256), 0, st, B.dx, B.dy, B.mag, B.map,
+                       P.H, P.W, P.canny_low, P.canny_high, ps); trace_point("k_nms", st);
     static const bool flat_uf = [] {
         const char* e = getenv("TSM_UF_FLAT");  // A/B: global-memory union-find over every pair
         return e && e[0] == '1';
     }();
     if (flat_uf) {
-        hipLaunchKernelGGL(k_uf_init, dim3((n + 255) / 256), dim3(256), 0, st, B.map, B.label, n); trace_point("k_uf_init", st);
-        hipLaunchKernelGGL(k_uf_merge, grid2d(P.W, P.H, 256), dim3(256), 0, st, B.map, B.label, P.H, P.W); trace_point("k_uf_merge", st);
+        hipLaunchKernelGGL(k_uf_init, grid1d((n + 255) / 256, P), dim3(256), 0, st, B.map, B.label, n, ps); trace_point("k_uf_init", st);
+        hipLaunchKernelGGL(k_uf_merge, grid2d(P.W, P.H, 256, P), dim3(256), 0, st, B.map, B.label, P.H, P.W, ps); trace_point("k_uf_merge", st);
     } else {
-        hipLaunchKernelGGL(k_uf_tile, dim3((P.W + UT - 1) / UT, (P.H + UT - 1) / UT), dim3(256), 0, st, B.map,
-                           B.label, P.H, P.W); trace_point("k_uf_tile", st);
-        hipLaunchKernelGGL(k_uf_edges, grid2d(P.W, P.H, 256), dim3(256), 0, st, B.map, B.label, P.H, P.W); trace_point("k_uf_edges", st);
+        hipLaunchKernelGGL(k_uf_tile, dim3((P.W + UT - 1) / UT, (P.H + UT - 1) / UT, P.npairs), dim3(256), 0, st, B.map,
+                           B.label, P.H, P.W, ps); trace_point("k_uf_tile", st);
+        hipLaunchKernelGGL(k_uf_edges, grid2d(P.W, P.H, 256, P), dim3(256), 0, st, B.map, B.label, P.H, P.W, ps); trace_point("k_uf_edges", st);
     }
-    hipLaunchKernelGGL(k_zero_u32, dim3((n / 4 + 256) / 256), dim3(256), 0, st, reinterpret_cast<uint32_t*>(B.strong), (n + 3) / 4); trace_point("k_zero_u32", st);
-    hipLaunchKernelGGL(k_uf_flatten_mark, dim3((n + 255) / 256), dim3(256), 0, st, B.map, B.label, B.strong, n); trace_point("k_uf_flatten_mark", st);
-    hipLaunchKernelGGL(k_uf_final, dim3((n + 255) / 256), dim3(256), 0, st, B.map, B.label, B.strong, B.edges, n); trace_point("k_uf_final", st);
-    hipLaunchKernelGGL(k_adjust, grid2d(P.W, P.H, 256), dim3(256), 0, st, B.dm, B.dtmp, B.edges, vol0, P); trace_point("k_adjust", st);
+    hipLaunchKernelGGL(k_zero_u32, grid1d((n / 4 + 256) / 256, P), dim3(256), 0, st, reinterpret_cast<uint32_t*>(B.strong), (n + 3) / 4, ps); trace_point("k_zero_u32", st);
+    hipLaunchKernelGGL(k_uf_flatten_mark, grid1d((n + 255) / 256, P), dim3(256), 0, st, B.map, B.label, B.strong, n, ps); trace_point("k_uf_flatten_mark", st);
+    hipLaunchKernelGGL(k_uf_final, grid1d((n + 255) / 256, P), dim3(256), 0, st, B.map, B.label, B.strong, B.edges, n, ps); trace_point("k_uf_final", st);
+    hipLaunchKernelGGL(k_adjust, grid2d(P.W, P.H, 256, P), dim3(256), 0, st, B.dm, B.dtmp, B.edges, vol0, P); trace_point("k_adjust", st);
     std::swap(B.dm, B.dtmp);
 }
 
 void launch_subpixel_median(const RefineBufs& B, const float* vol0, const uint32_t* orig_left,
-                            float* out, size_t out_step, int roi_or_mask, int offset,
+                            const PairOut& outs, size_t out_step, int roi_or_mask, int offset,
                             const DevParams& P, hipStream_t st) {
-    hipLaunchKernelGGL(k_subpix, grid2d(P.W, P.H, 256), dim3(256), 0, st, B.dm, vol0, B.subpix, P); trace_point("k_subpix", st);
-    hipLaunchKernelGGL(k_median_out, grid2d(P.W, P.H, 256), dim3(256), 0, st, B.subpix, out,
-                       out_step, orig_left, roi_or_mask, offset, P.H, P.W); trace_point("k_median_out", st);
+    hipLaunchKernelGGL(k_subpix, grid2d(P.W, P.H, 256, P), dim3(256), 0, st, B.dm, vol0, B.subpix, P); trace_point("k_subpix", st);
+    hipLaunchKernelGGL(k_median_out, grid2d(P.W, P.H, 256, P), dim3(256), 0, st, B.subpix, outs,
+                       out_step, orig_left, roi_or_mask, offset, P.H, P.W, P.pstride); trace_point("k_median_out", st);
 }
 
 void launch_vol_to_ref(const float* vol, float* ref, int views, const DevParams& P, hipStream_t st) {

@@ -293,6 +293,7 @@ __global__ __launch_bounds__(256) void k_scan_line(float* __restrict__ vol,
     const int H = P.H, W = P.W, Lp = P.Lp;
     const int lane = threadIdx.x & 63;
     const int line = __builtin_amdgcn_readfirstlane(blockIdx.x * 4 + (threadIdx.x >> 6));
+    pair_shift(blockIdx.z, P.pstride, vol, grad, img, wta);  // infvec: shared, not per pair
     const int v = blockIdx.y;
     if (line >= (HORIZ ? H : W)) return;
     const ScanConst C = scan_const(P);
@@ -450,7 +451,7 @@ __global__ __launch_bounds__(256) void k_scan_line(float* __restrict__ vol,
 template <int J, bool HORIZ, bool MASK, bool WTA>
 static void launch_scan_t(float* vol, const uint8_t* grad, const uint32_t* img, int dir, int32_t* wta,
                           int store_view1, const float* infvec, const DevParams& P, hipStream_t st) {
-    dim3 g(((HORIZ ? P.H : P.W) + 3) / 4, 2);
+    dim3 g(((HORIZ ? P.H : P.W) + 3) / 4, 2, P.npairs);
     if (P.omp_threads > 1)
         hipLaunchKernelGGL((k_scan_line<J, HORIZ, MASK, WTA, true>), g, dim3(256), 0, st, vol, grad, img, dir,
                            wta, store_view1, infvec, P);
@@ -504,6 +505,7 @@ __global__ __launch_bounds__(256) void k_wta(const float* __restrict__ vol, int3
     const DevParams P = Pk;
     const int lane = threadIdx.x & 63;
     const size_t npx = (size_t)2 * P.H * P.W;
+    pair_shift(blockIdx.z, P.pstride, vol, disp);
     const size_t g0 = ((size_t)blockIdx.x * 4 + (threadIdx.x >> 6)) * WTA_PX;
     if (g0 >= npx) return;
     const int Q = P.Lp >> 2;
@@ -530,7 +532,7 @@ __global__ __launch_bounds__(256) void k_wta(const float* __restrict__ vol, int3
 int launch_wta(const float* vol, int32_t* disp, const float* infvec, const DevParams& P, hipStream_t st) {
     const int J = (P.Lp / 4 + 63) / 64;
     const size_t npx = (size_t)2 * P.H * P.W;
-    const dim3 g((unsigned)((npx + 4 * WTA_PX - 1) / (4 * WTA_PX)));
+    const dim3 g((unsigned)((npx + 4 * WTA_PX - 1) / (4 * WTA_PX)), 1, P.npairs);
     if (J == 1) hipLaunchKernelGGL((k_wta<1>), g, dim3(256), 0, st, vol, disp, infvec, P);
     else if (J == 2) hipLaunchKernelGGL((k_wta<2>), g, dim3(256), 0, st, vol, disp, infvec, P);
     else return -1;

@@ -45,7 +45,36 @@ struct DevParams {
     int canny_low, canny_high;
     int omp_threads;   // scanline race emulation (0/1 = serial semantics)
     int gpad, gstride; // colour-difference maps: row stride and left margin (sentinel bytes)
+    // Pair groups: a launch runs `npairs` pairs; pair p's per-pair buffers sit p * pstride
+    // bytes past pair 0's (one arena, one slot per pair), and every kernel takes its pair
+    // from blockIdx.z (kernels with a view axis: blockIdx.z = 2 * pair + view).
+    size_t pstride;
+    int npairs;
 };
+
+// Largest group a launch carries (pointer tables of per-pair user buffers are kernel
+// arguments of this many entries).
+constexpr int kMaxGroup = 16;
+
+// Per-pair user buffers of a group (inputs, outputs), passed by value.
+struct PairIn {
+    const uint8_t* left[kMaxGroup];
+    const uint8_t* right[kMaxGroup];
+};
+struct PairOut {
+    float* out[kMaxGroup];
+};
+
+// Move arena pointers from pair 0's slot to pair `pair`'s (null pointers stay null).
+template <class Ptr>
+__device__ __forceinline__ void pair_shift1(size_t off, Ptr& p) {
+    if (p) p = (Ptr)(reinterpret_cast<uintptr_t>(p) + off);
+}
+template <class... Ptr>
+__device__ __forceinline__ void pair_shift(unsigned pair, size_t pstride, Ptr&... p) {
+    const size_t off = (size_t)pair * pstride;
+    (pair_shift1(off, p), ...);
+}
 
 // Left/right margin of the colour-difference maps gv/gh: a scanline step reads 4
 // consecutive bytes at x = line +- (d + minD), d < L, through an aligned 8-byte load.

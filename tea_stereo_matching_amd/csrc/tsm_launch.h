@@ -13,9 +13,9 @@ namespace tsm {
 void trace_point(const char* what, hipStream_t st);
 
 // k_cost.hip
-void launch_pack(const uint8_t* left, const uint8_t* right, size_t step, int H, int W,
-                 uint32_t* img, hipStream_t st);
-void launch_hsi(const uint32_t* src, uint32_t* tmp, uint32_t* dst, int H, int W, int filter,
+// Every launcher runs its stage for the group's P.npairs pairs (DevParams.pstride apart).
+void launch_pack(const PairIn& in, size_t step, uint32_t* img, const DevParams& P, hipStream_t st);
+void launch_hsi(const uint32_t* src, uint32_t* tmp, uint32_t* dst, int filter, const DevParams& P,
                 hipStream_t st);
 void launch_census(const uint32_t* img, uint32_t* desc, const DevParams& P, hipStream_t st);
 size_t cost_volume_lds_bytes(const DevParams& P, int lutA_n);
@@ -85,10 +85,10 @@ void launch_interpolation(RefineBufs& B, const uint32_t* img0, const DevParams& 
 void launch_discontinuity(RefineBufs& B, const float* vol0, const DevParams& P,
                           hipStream_t st);
 void launch_subpixel_median(const RefineBufs& B, const float* vol0, const uint32_t* orig_left,
-                            float* out, size_t out_step, int roi_or_mask, int offset,
+                            const PairOut& outs, size_t out_step, int roi_or_mask, int offset,
                             const DevParams& P, hipStream_t st);
 
-// debug helpers
+// debug helpers (pair 0 of the group)
 void launch_vol_to_ref(const float* vol, float* ref, int views, const DevParams& P,
                        hipStream_t st);
 void launch_arms_to_ref(const uint32_t* arms, int32_t* ref, const DevParams& P, hipStream_t st);

@@ -151,13 +151,14 @@ def test_batch_device_rejects_null_or_short_output(matcher, tsm, hip):
 
 
 def test_batch_host_error_midway_drains_queued_pairs(matcher, tsm):
-    """An invalid pair inside tsm_adc_compute_batch returns its error after the pairs
-    already enqueued have finished (their host buffers are safe to free)."""
+    """An invalid pair inside tsm_adc_compute_batch returns its error after the groups
+    already enqueued have finished (their host buffers are safe to free): with groups of
+    two, pairs 0-1 run as the first group and the second group (pair 2) is refused."""
     H, W = 40, 64
     pairs = [tsm.synthetic.make_scene(300 + i, H, W, 17)[:2] for i in range(3)]
     matcher.setMatchingStrategy(tsm.ColorModel.RGB)
     matcher.setMinMaxDisparity(0, 16)
-    matcher.setConcurrency(3)
+    matcher.setConcurrency(2)
     from tea_stereo_matching_amd import _native as N
 
     lib = N.load()

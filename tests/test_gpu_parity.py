@@ -194,6 +194,33 @@ def test_batch_equals_single(matcher, tsm):
         assert np.array_equal(o, matcher.compute(l, r))
 
 
+@pytest.mark.parametrize("mode", ["hsi", "mask", "census7x5", "minD"])
+def test_group_equals_single(matcher, tsm, mode):
+    """A group of pairs (one pipeline, every launch over the group's pair slots) gives each
+    pair exactly its single-pair result, in every model / mode."""
+    H, W = 56, 88
+    pairs = [_synthetic(tsm, 400 + i, H, W, 33) for i in range(4)]
+    if mode == "mask":
+        for l, r in pairs:
+            l[:, :7] = 0
+            r[:, -5:] = 0
+    model = tsm.ColorModel.HSI if mode == "hsi" else tsm.ColorModel.RGB
+    matcher.setMatchingStrategy(model, False, mode == "mask")
+    if mode == "census7x5":
+        p = matcher.params()
+        p.census_win = 1
+        matcher.setParams(p)
+    matcher.setMinMaxDisparity(3 if mode == "minD" else 0, 32)
+    matcher.setOmpEmulation(0)
+    singles = [matcher.compute(l, r) for l, r in pairs]
+    for conc in (4, 3):
+        matcher.setConcurrency(conc)
+        outs = matcher.compute_batch([p[0] for p in pairs], [p[1] for p in pairs])
+        for o, s1 in zip(outs, singles):
+            assert np.array_equal(o, s1)
+    matcher.setMatchingStrategy(tsm.ColorModel.RGB)
+
+
 def test_api_errors_match_reference(matcher, tsm):
     E = tsm.ADCensusError
     with pytest.raises(E, match=r"^\[ADCensus\] Set MinMaxDisparity error\.$"):
