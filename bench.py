@@ -11,11 +11,15 @@ disparity maps over RCCL.  Weak scaling: per-GPU work is fixed as N grows.
   python bench.py [--gpus N --steps K --warmup W]
   python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N ...
 
+The library runs a batch in groups of `--concurrency` pairs: one pipeline per group whose
+every launch covers the group's pairs (pair slots of one HBM arena), so the row-serial
+scanline passes and the latency-bound refinement kernels are paid once per group.
+
 Rank 0 prints ONE JSON line.  `roofline` prices the kernel named by BASELINE.json (the
 cost-volume build) from HIP events around its launches on the pipeline's stream, in an
-untimed phase after the timed region where one pipeline runs alone (in the timed region
-`--concurrency` pipelines overlap, so a kernel's event span would include its
-neighbours' work); `next_rows` times the f2-f4 operators on the pipeline's outputs;
+untimed phase after the timed region where pairs run one at a time (groups of one: each
+cost launch covers exactly one pair and runs alone); `next_rows` times the f2-f4
+operators on the pipeline's outputs;
 `cpu_baseline` times the oracle (the C restatement of the reference's OpenMP path)
 on one pair on this host's cores.
 """
@@ -39,8 +43,9 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=2)
-    ap.add_argument("--batch", type=int, default=8, help="pairs per GPU per step")
-    ap.add_argument("--concurrency", type=int, default=8, help="pair pipelines in flight per GPU")
+    ap.add_argument("--batch", type=int, default=64, help="pairs per GPU per step")
+    ap.add_argument("--concurrency", type=int, default=32,
+                    help="pairs per group (one pipeline per group; consecutive groups run on two streams)")
     ap.add_argument("--height", type=int, default=375)
     ap.add_argument("--width", type=int, default=1242)
     ap.add_argument("--max-disparity", type=int, default=192)
@@ -187,6 +192,7 @@ def main():
             "pairs_per_gpu_per_step": B,
             "global_batch": world * B,
             "concurrency": args.concurrency,
+            "pipeline": f"groups of {args.concurrency} pairs (one launch per stage per group), consecutive groups on two streams",
             "parallelism": f"dp{world} (pairs sharded, RCCL gather to rank 0)" if world > 1 else "dp1",
             "gather": world > 1 and not args.no_gather,
         },

@@ -144,7 +144,7 @@ int tsm_adc_synchronize(tsm_adc* h);
 int tsm_adc_get_params(const tsm_adc* h, tsm_adc_params* out);
 int tsm_adc_set_params(tsm_adc* h, const tsm_adc_params* in);
 int tsm_adc_get_disparity_range(const tsm_adc* h, int* min_disparity, int* max_disparity);
-/* Pairs per group in the batch entry points (default 2, at most 16): a group of K pairs
+/* Pairs per group in the batch entry points (default 2, at most 64): a group of K pairs
  * runs as one pipeline whose every launch covers the K pairs (K pair slots in one arena),
  * and consecutive groups alternate between two streams. */
 int tsm_adc_set_concurrency(tsm_adc* h, int n_streams);

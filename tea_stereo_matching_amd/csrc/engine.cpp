@@ -119,6 +119,8 @@ struct Workspace {
     // profiling: per group, its stage events and pair count
     std::vector<hipEvent_t> ev_pool;
     std::vector<std::pair<std::vector<hipEvent_t>, int>> pending;
+    // recorded at the group's stagger point (see group_stagger): the next group starts there
+    hipEvent_t stagger_evt = nullptr;
 };
 
 }  // namespace
@@ -322,6 +324,7 @@ DevParams make_params(const tsm_adc* h, int H, int W) {
 int ensure_workspace(tsm_adc* h, Workspace* w, int H, int W, int K) {
     const int L = h->max_disparity - h->min_disparity + 1;
     if (w->stream == nullptr) HIP_OK(hipStreamCreateWithFlags(&w->stream, hipStreamNonBlocking));
+    if (w->stagger_evt == nullptr) HIP_OK(hipEventCreateWithFlags(&w->stagger_evt, hipEventDisableTiming));
     const tsm_adc_params& p = h->params;
     if (w->H == H && w->W == W && w->L == L && w->maxD == h->max_disparity && w->model == h->color_model &&
         w->lambda_ad == p.lambda_ad && w->lambda_census == p.lambda_census && w->cap >= K)
@@ -440,6 +443,20 @@ hipEvent_t take_event(Workspace* w) {
     return e;
 }
 
+// Where a batch's next group may start on its own stream (TSM_GROUP_STAGGER): after the
+// cost volume (2), the aggregation (4) or the scanline (5) of the group before it, or at
+// once (0, default).  Measured on config B, batch 64 in groups of 32: lock step 359
+// pairs/s, staggered after the cost 355, after the aggregation 339, after the scanline
+// 342 -- the two groups gain most by filling each other's kernel tails, not by pairing
+// a bandwidth-bound head with a latency-bound tail.
+int group_stagger() {
+    static const int v = [] {
+        const char* e = getenv("TSM_GROUP_STAGGER");
+        return e ? atoi(e) : 0;
+    }();
+    return v;
+}
+
 // Enqueue the full pipeline for a group of K pairs on workspace w (K <= w->cap).
 // in: device BGR images with `step`; outs: device fp32 maps with out_step.  Every launch
 // covers the K pairs.  No host synchronisation (dumps, K = 1 only, synchronise).
@@ -474,24 +491,31 @@ int run_pipeline(tsm_adc* h, Workspace* w, int K, const PairIn& in, size_t step,
         return TSM_OK;
     };
     int rc;
+    // stagger point: after the stage this many marks in (0 = none)
+    int nmark = 0;
+    const int stagger = group_stagger();
+    auto mark_stage = [&]() {
+        mark();
+        if (stagger > 0 && ++nmark == stagger + 1 && w->stagger_evt) hipEventRecord(w->stagger_evt, st);
+    };
 #ifdef TSM_EXP_SKIP
     static const int skip = [] { const char* e = getenv("TSM_SKIP"); return e ? atoi(e) : 0; }();
 #else
     constexpr int skip = 0;
 #endif
 
-    mark();
+    mark_stage();
     // --- prep: pack (+HSI), census descriptors -------------------------------------
     launch_pack(in, step, w->img_orig, P, st);
     if (h->color_model == TSM_COLOR_HSI)
         launch_hsi(w->img_orig, w->img_tmp, w->img, (h->roi || h->mask) ? 1 : 0, P, st);
     launch_census(w->img, w->desc, P, st);
-    mark();
+    mark_stage();
     // --- cost volume -------------------------------------------------------------
     if (!(skip & 16) && launch_cost_volume(w->img, w->desc, w->lutA, w->lutA_n, w->lutB, w->vol, P, w->cost_ctr,
                            w->cost_ctr_base, st) != 0)
         return fail(h, TSM_ERR_UNSUPPORTED, "cost volume: label count");
-    mark();
+    mark_stage();
     if (dump && dump->images) {
         std::vector<uint32_t> tmp(2 * N);
         if ((rc = d2h(tmp.data(), w->img, 2 * N * 4)) != TSM_OK) return rc;
@@ -506,7 +530,7 @@ int run_pipeline(tsm_adc* h, Workspace* w, int K, const PairIn& in, size_t step,
     launch_arms(w->img, w->arms, P, st);
     launch_window_sizes(w->arms, w->ws, P, st);
     launch_color_grad(w->img, w->gv, w->gh, P, st);
-    mark();
+    mark_stage();
     if (dump && dump->arms) {
         int32_t* tmp = nullptr;
         HIP_OK(hipMalloc((void**)&tmp, 8 * N * 4));
@@ -548,7 +572,7 @@ int run_pipeline(tsm_adc* h, Workspace* w, int K, const PairIn& in, size_t step,
             if (rcp != 0) return fail(h, TSM_ERR_UNSUPPORTED, "aggregation: label count");
         }
     }
-    mark();
+    mark_stage();
     if (dump && dump->cost_agg && (rc = dump_vol(dump->cost_agg, 2)) != TSM_OK) return rc;
     // --- scanline, then WTA of both final volumes --------------------------------------
     const bool keep_view1 = dump && dump->cost_scan;
@@ -569,11 +593,11 @@ int run_pipeline(tsm_adc* h, Workspace* w, int K, const PairIn& in, size_t step,
         ok = launch_scan_horizontal(w->vol, w->gh, w->img, -1, nullptr, 1, w->infvec, P, st) == 0 &&
              launch_wta(w->vol, w->rb.disp0, w->infvec, P, st) == 0;
     if (!ok) return fail(h, TSM_ERR_UNSUPPORTED, "scanline: label count");
-    mark();
+    mark_stage();
     if (keep_view1 && (rc = dump_vol(dump->cost_scan, 2)) != TSM_OK) return rc;
     if (dump && dump->wta && (rc = d2h(dump->wta, w->rb.disp0, 2 * N * 4)) != TSM_OK) return rc;
     // --- refinement --------------------------------------------------------------------
-    if (skip & 1) { mark(); mark(); HIP_OK(hipGetLastError()); if (h->profiling) w->pending.emplace_back(ev, K); return TSM_OK; }
+    if (skip & 1) { mark_stage(); mark_stage(); HIP_OK(hipGetLastError()); if (h->profiling) w->pending.emplace_back(ev, K); return TSM_OK; }
     launch_outlier(w->rb, P, st);
     if (dump && dump->outlier && (rc = d2h(dump->outlier, w->rb.dm, N * 4)) != TSM_OK) return rc;
     {
@@ -593,7 +617,7 @@ int run_pipeline(tsm_adc* h, Workspace* w, int K, const PairIn& in, size_t step,
     launch_subpixel_median(w->rb, w->vol, w->img_orig, outs, out_step, (h->roi || h->mask) ? 1 : 0,
                            h->offset, P, st);
     if (dump && dump->subpix && (rc = d2h(dump->subpix, w->rb.subpix, N * 4)) != TSM_OK) return rc;
-    mark();
+    mark_stage();
     HIP_OK(hipGetLastError());
     if (h->profiling) w->pending.emplace_back(ev, K);
     return TSM_OK;
@@ -677,6 +701,7 @@ int tsm_adc_destroy(tsm_adc* h) {
         for (auto& pe : w->pending) for (hipEvent_t e : pe.first) hipEventDestroy(e);
         for (hipEvent_t e : w->ev_pool) hipEventDestroy(e);
         if (w->stream) hipStreamDestroy(w->stream);
+        if (w->stagger_evt) hipEventDestroy(w->stagger_evt);
         delete w;
     }
     delete h;
@@ -734,7 +759,7 @@ int tsm_adc_set_params(tsm_adc* h, const tsm_adc_params* in) {
 }
 
 int tsm_adc_set_concurrency(tsm_adc* h, int n) {
-    if (!h || n < 1 || n > 16) return TSM_ERR_ARGUMENT;
+    if (!h || n < 1 || n > kMaxGroup) return TSM_ERR_ARGUMENT;
     h->concurrency = n;
     return TSM_OK;
 }
@@ -867,9 +892,23 @@ int tsm_adc_compute_debug(tsm_adc* h, const uint8_t* l, const uint8_t* r, int ro
 // workspaces (two streams) when there is more than one group.  K = 1 keeps one
 // workspace: pairs then run strictly one after another (per-stage timing alone).
 static int group_plan(tsm_adc* h, int n, int& K, int& nws) {
+    static const int streams = [] {  // group workspaces in rotation (tuning: TSM_GROUP_STREAMS)
+        const char* e = getenv("TSM_GROUP_STREAMS");
+        const int v = e ? atoi(e) : 2;
+        return v < 1 ? 1 : (v > 4 ? 4 : v);
+    }();
     K = std::min(h->concurrency, kMaxGroup);
-    nws = (n > K && K > 1) ? 2 : 1;
+    nws = (n > K && K > 1) ? std::min(streams, (n + K - 1) / K) : 1;
     return ensure_pool(h, nws);
+}
+
+// Group g's stream waits for group g-1's stagger point (other workspace's stream).
+static int wait_previous_group(tsm_adc* h, int g, int nws) {
+    if (g == 0 || nws < 2 || group_stagger() <= 0) return TSM_OK;
+    Workspace* prev = h->ws[(g - 1) % nws];
+    Workspace* w = h->ws[g % nws];
+    HIP_OK(hipStreamWaitEvent(w->stream, prev->stagger_evt, 0));
+    return TSM_OK;
 }
 
 int tsm_adc_compute_batch_device(tsm_adc* h, int n, const uint8_t* const* dls,
@@ -888,6 +927,7 @@ int tsm_adc_compute_batch_device(tsm_adc* h, int n, const uint8_t* const* dls,
         const int k = std::min(K, n - i0);
         Workspace* w = h->ws[g % nws];
         if ((rc = ensure_workspace(h, w, rows, cols, K)) != TSM_OK) return drain_after_error(h, rc);
+        if ((rc = wait_previous_group(h, g, nws)) != TSM_OK) return drain_after_error(h, rc);
         PairIn in{};
         PairOut out{};
         for (int j = 0; j < k; ++j) {
@@ -920,6 +960,7 @@ int tsm_adc_compute_batch(tsm_adc* h, int n, const uint8_t* const* ls, const uin
         if ((rc = ensure_workspace(h, w, rows, cols, K)) != TSM_OK) return drain_after_error(h, rc);
         if ((rc = ensure_input_staging(h, w, rows, (size_t)cols * 3, cols, K)) != TSM_OK)
             return drain_after_error(h, rc);
+        if ((rc = wait_previous_group(h, g, nws)) != TSM_OK) return drain_after_error(h, rc);
         PairIn in{};
         PairOut po{};
         for (int j = 0; j < k; ++j) {

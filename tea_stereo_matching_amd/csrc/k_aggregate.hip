@@ -1236,6 +1236,272 @@ __global__ __launch_bounds__(AX_THREADS) void k_agg_split(AggStream S, DevParams
     AST_FLUSH();
 }
 
+// ---------------------------------------------------------------------------
+// 1-D aggregation v7: the v6 role split with scalar-lean steps (the default)
+// ---------------------------------------------------------------------------
+// Same stream, rings, descriptors and roles as v6 (k_agg_split).  v6 is bound by the
+// CU's single scalar unit: its 16 waves decode descriptors, loop over window blocks and
+// track load positions in SGPRs (PMC: 1.7 scalar per vector instruction; with no HBM
+// traffic at all the five launches still take 1.31 ms a pair).  Here every per-pixel
+// quantity is a VGPR (descriptor decode, ring offsets, load offsets: uniform values
+// kept per lane behind an opaque move), and a window of up to 8 ring pixels is summed
+// without a loop: two blocks of 4 reads go out together and a read past the window is
+// added as fma(x, 0, acc) == acc (fma(x, 1, acc) == acc + x: one rounding, the same
+// value as the reference's add; every slot read holds a finite cost, or padding, whose
+// NaN can only land in padding labels, which every consumer ignores).  The rings are
+// zeroed once so no uninitialised LDS is ever read.  Lanes past the label vector work on
+// the last lane's slot (identical values), so LDS writes need no exec mask.  What stays
+// scalar: the window-length class branch, line changes, the B store's validity.
+__device__ __forceinline__ uint32_t vopaque(uint32_t x) {
+    asm volatile("" : "+v"(x));
+    return x;
+}
+__device__ __forceinline__ f32x4 fmam(f32x4 acc, f32x4 x, float m) {
+    return __builtin_elementwise_fma(x, f32x4{m, m, m, m}, acc);
+}
+// 1 if k < len else 0 (len, k small non-negative integers as floats)
+__device__ __forceinline__ float wmask(float lenf, float k) { return __builtin_amdgcn_fmed3f(lenf - k, 0.f, 1.f); }
+
+template <bool FUSED, bool DIV, int QT>
+__global__ __launch_bounds__(AX_THREADS) void k_agg_v7(AggStream S, DevParams Pk) {
+    const DevParams P = Pk;
+    pair_shift(blockIdx.z, P.pstride, S.vol, S.arms, S.ws, S.pk, S.rcp);
+    extern __shared__ __attribute__((aligned(16))) f32x4 smem_f4[];
+    const int H = P.H, W = P.W, Lp = P.Lp;
+    const int slice = blockIdx.y;
+    const int Q = QT > 0 ? QT : (slice == 0 ? S.qn0 : S.qtot - S.qn0);
+    float* const volq = S.vol + 4 * (slice == 0 ? 0 : S.qn0);
+    const uint32_t Qs = (uint32_t)Q * 16;
+    const size_t vstride = (size_t)H * W * Lp;
+    const size_t es = S.horizontal ? (size_t)Lp : (size_t)W * Lp;
+    const size_t ls = S.horizontal ? (size_t)W * Lp : (size_t)Lp;
+    const size_t aes = S.horizontal ? 1 : (size_t)W;
+    const size_t als = S.horizontal ? (size_t)W : 1;
+    const int g = blockIdx.x, G = gridDim.x;
+    const int my_lines = (S.nl - g + G - 1) / G;
+    const int nch = my_lines * S.cpl;
+    const uint32_t r2_off = (uint32_t)(AS_RP1 + AX_MIR) * Qs;
+    const uint32_t meta_off = r2_off + (uint32_t)(AS_RP2 + AX_MIR) * Qs;
+    const uint32_t span1 = (uint32_t)AS_RP1 * Qs, span2 = (uint32_t)AS_RP2 * Qs;
+    char* lds = reinterpret_cast<char*>(smem_f4);
+    const int tid = threadIdx.x;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int lane = tid & 63;
+    const bool roleA = wave < AS_SEG;
+    const int w = roleA ? wave : wave - AS_SEG;
+    const int nsteps = nch + (FUSED ? AS_LAG : 1);
+    const int nblk = (nsteps + AX_D - 1) / AX_D;
+    const bool vl = lane < Q;
+    const int lanec = vl ? lane : Q - 1;
+    const uint32_t lc16 = (uint32_t)lanec * 16;
+    const uint32_t mstep = AS_SEG * AX_MW * 4;
+    auto barrier = [&]() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); };
+    // zero both rings (and their mirror slots): masked window reads never see garbage
+    for (uint32_t o = (uint32_t)tid * 16; o < meta_off; o += AX_THREADS * 16)
+        *reinterpret_cast<f32x4*>(lds + o) = f32x4{0.f, 0.f, 0.f, 0.f};
+    barrier();
+    // sequential window sum of `len` ring pixels starting at ring-relative byte offset `rel`
+    // (a VGPR) of the ring at `base` (lds + ring offset + this lane's 16 B) of `span` bytes
+    auto window = [&](const char* base, uint32_t rel, uint32_t len_v, int len, uint32_t span) -> f32x4 {
+        const float lenf = (float)len_v;
+        const char* p = base + rel;
+        const f32x4 x0 = *reinterpret_cast<const f32x4*>(p);
+        const f32x4 x1 = *reinterpret_cast<const f32x4*>(p + Qs);
+        const f32x4 x2 = *reinterpret_cast<const f32x4*>(p + 2 * Qs);
+        const f32x4 x3 = *reinterpret_cast<const f32x4*>(p + 3 * Qs);
+        if (len <= 4) {
+            f32x4 acc = x0;
+            acc = fmam(acc, x1, wmask(lenf, 1.f));
+            acc = fmam(acc, x2, wmask(lenf, 2.f));
+            acc = fmam(acc, x3, wmask(lenf, 3.f));
+            return acc;
+        }
+        uint32_t r1 = rel + 4 * Qs;
+        r1 = min(r1, r1 - span);  // wrap (ring-relative offsets: the subtraction underflows unless r1 >= span)
+        const char* q = base + r1;
+        const f32x4 x4 = *reinterpret_cast<const f32x4*>(q);
+        const f32x4 x5 = *reinterpret_cast<const f32x4*>(q + Qs);
+        const f32x4 x6 = *reinterpret_cast<const f32x4*>(q + 2 * Qs);
+        const f32x4 x7 = *reinterpret_cast<const f32x4*>(q + 3 * Qs);
+        f32x4 acc = x0;
+        acc += x1;
+        acc += x2;
+        acc += x3;
+        acc += x4;
+        acc = fmam(acc, x5, wmask(lenf, 5.f));
+        acc = fmam(acc, x6, wmask(lenf, 6.f));
+        acc = fmam(acc, x7, wmask(lenf, 7.f));
+        if (len > 8) {  // long windows (rare on natural images): blocks of 4, masked tail
+            uint32_t r = r1 + 4 * Qs;
+            r = min(r, r - span);
+            for (int done = 8; done < len; done += 4) {
+                const char* t = base + r;
+                const f32x4 y0 = *reinterpret_cast<const f32x4*>(t);
+                const f32x4 y1 = *reinterpret_cast<const f32x4*>(t + Qs);
+                const f32x4 y2 = *reinterpret_cast<const f32x4*>(t + 2 * Qs);
+                const f32x4 y3 = *reinterpret_cast<const f32x4*>(t + 3 * Qs);
+                const float d = (float)done;
+                acc += y0;
+                acc = fmam(acc, y1, wmask(lenf, d + 1.f));
+                acc = fmam(acc, y2, wmask(lenf, d + 2.f));
+                acc = fmam(acc, y3, wmask(lenf, d + 3.f));
+                r += 4 * Qs;
+                r = min(r, r - span);
+            }
+        }
+        return acc;
+    };
+    // ring-relative byte offset of the window start of pixel `slot` (ring pixel index)
+    // with left arm lo, in a ring of `span` bytes: (slot - lo) * Qs, wrapped
+    auto wstart = [&](uint32_t slotQs, uint32_t lo, uint32_t span) -> uint32_t {
+        const uint32_t t = slotQs - lo * Qs;
+        return min(t, t + span);
+    };
+    const char* mbase = lds + meta_off + (uint32_t)w * AX_MW * 4;  // this wave's pixel column of the meta ring
+
+    if (roleA) {
+        // ---- A: staging ring, land, pass A ----------------------------------------------
+        const __amdgpu_buffer_rsrc_t rs_vol = make_rsrc(volq), rs_pk = make_rsrc(S.pk),
+                                     rs_rcp = make_rsrc(S.rcp);
+        const uint32_t es4 = (uint32_t)(es * 4), aes4 = (uint32_t)(aes * 4);
+        // issue position (chunk ci = s + AHEAD + AX_D at step s), advanced one chunk a step
+        int il = 0, icc = 0;
+        uint32_t iv = 0, ia = 0;  // byte offsets of line il: vol, descriptors (= reciprocals)
+        auto set_line = [&]() {
+            const int gl = g + il * G;
+            const int v = gl / S.nlv, line = gl - v * S.nlv;
+            iv = (uint32_t)(((size_t)v * vstride + (size_t)line * ls) * 4);
+            ia = (uint32_t)(2 * v * H * W + line * (int)als) * 4;  // per-view stride 2HW
+        };
+        set_line();
+        const uint32_t wv = vopaque((uint32_t)w), lastpx = vopaque((uint32_t)(S.n - 1));
+        f32x4 rv[AX_D];
+        uint32_t rma[AX_D], rmy[AX_D];  // packed descriptor, RN(1/size) bits
+        auto issue = [&](int k) {  // chunk at (il, icc) -> slot k; past the end: re-read the last pixel
+            const bool past = il >= my_lines;
+            // position and offsets in VGPRs (the SGPRs only track the line)
+            const uint32_t pos = past ? lastpx : min((uint32_t)(icc * AS_SEG) + wv, lastpx);
+            const uint32_t vo = iv + pos * es4 + lc16, mo = ia + pos * aes4;
+#ifdef TSM_EXP_AGG_NOLOAD
+            rv[k] = f32x4{(float)vo, 0.f, 0.f, 0.f};  // timing experiment only
+#else
+            rv[k] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rs_vol, vo, 0, 0));
+#endif
+            rma[k] = (uint32_t)__builtin_amdgcn_raw_buffer_load_b32(rs_pk, mo, 0, 0);
+            rmy[k] = DIV ? (uint32_t)__builtin_amdgcn_raw_buffer_load_b32(rs_rcp, mo, 0, 0) : 0u;
+            if (!past && ++icc == S.cpl) {
+                icc = 0;
+                ++il;
+                if (il < my_lines) set_line();
+            }
+        };
+        char* const r1w = lds + (uint32_t)w * Qs + lc16;            // ring1, this wave's pixel column
+        const char* const r1b = lds + lc16;                         // ring1 window base
+        char* const r2w = lds + r2_off + (uint32_t)w * Qs + lc16;   // ring2, this wave's pixel column
+        // pixel w of chunk c -> ring1; its raw descriptor -> the meta ring
+        auto land = [&](const f32x4& val, uint32_t ma, uint32_t my, int c) {
+            const int cs = (c % AS_RC1) * AS_SEG;  // chunk slot (pixel index of its pixel 0)
+            *reinterpret_cast<f32x4*>(r1w + (uint32_t)cs * Qs) = val;
+            if (cs == 0 && w < AX_MIR) *reinterpret_cast<f32x4*>(r1w + (uint32_t)AS_RP1 * Qs) = val;
+            *reinterpret_cast<u32x2*>(lds + meta_off + (uint32_t)((c % AX_MC) * AS_SEG + w) * AX_MW * 4) = u32x2{ma, my};
+        };
+        // prologue: chunks 0 .. AHEAD + AX_D - 1 in flight, chunks 0 .. AHEAD - 1 landed
+        f32x4 pre[AS_AHEAD];
+        uint32_t pma[AS_AHEAD], pmy[AS_AHEAD];
+#pragma unroll
+        for (int c = 0; c < AS_AHEAD; ++c) {
+            issue(0);
+            pre[c] = rv[0];
+            pma[c] = rma[0];
+            pmy[c] = rmy[0];
+        }
+#pragma unroll
+        for (int k = 0; k < AX_D; ++k) issue(k);
+#pragma unroll
+        for (int c = 0; c < AS_AHEAD; ++c) land(pre[c], pma[c], pmy[c], c);
+        barrier();
+        u32x2 mA = *reinterpret_cast<const u32x2*>(mbase);
+        for (int b = 0; b < nblk; ++b) {
+#pragma unroll
+            for (int u = 0; u < AX_D; ++u) {
+                const int s = b * AX_D + u;
+                // land chunk s + AHEAD from slot u, then refill the slot (chunk s + AHEAD + AX_D)
+                land(rv[u], rma[u], rmy[u], s + AS_AHEAD);
+                issue(u);
+                // pass A on chunk s, pixel w (ring1 slot u*8 + w): descriptor in VGPRs
+                const uint32_t pk = vopaque(mA.x);
+                const float a_y = __uint_as_float(vopaque(mA.y));
+                const uint32_t lo = pk & 0xffu, hi = (pk >> 8) & 0xffu;
+                const float a_b = (float)(pk >> 16);
+                const uint32_t len_v = lo + hi + 1;
+                const int len = (int)__builtin_amdgcn_readfirstlane(len_v);
+                const uint32_t rel = wstart((uint32_t)(u * AS_SEG) * Qs + wv * Qs, lo, span1);
+                mA = *reinterpret_cast<const u32x2*>(mbase + ((u + 1) % AX_MC) * mstep);  // chunk s + 1 (landed)
+                f32x4 acc = window(r1b, rel, len_v, len, span1);
+                if (DIV) acc = div_ws(acc, a_b, a_y);
+                // every step writes its ring2 slot (chunks past the stream are never read)
+                *reinterpret_cast<f32x4*>(r2w + (uint32_t)(u * AS_SEG) * Qs) = acc;
+                if (u == 0 && w < AX_MIR) *reinterpret_cast<f32x4*>(r2w + (uint32_t)AS_RP2 * Qs) = acc;
+                barrier();
+                (void)s;
+            }
+        }
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // no load outlives the workgroup
+        return;
+    }
+
+    // ---- B: pass B over ring2 (FUSED) or pass A's outputs out of ring2, stores ------------
+    auto line_base = [&](int lidx) -> size_t {
+        const int gl = g + lidx * G;
+        const int v = gl / S.nlv, line = gl - v * S.nlv;
+        return (size_t)v * vstride + (size_t)line * ls;
+    };
+    int o_l = 0, o_cc = 0;
+    size_t o_off = line_base(0) + (size_t)w * es;
+    constexpr int lag = FUSED ? AS_LAG : 1;
+    const uint32_t wv = vopaque((uint32_t)w);
+    const char* const r2b = lds + r2_off + lc16;
+    barrier();
+    uint32_t mB = *reinterpret_cast<const uint32_t*>(mbase + ((AX_D - lag) % AX_MC) * mstep);  // chunk -lag
+    for (int b = 0; b < nblk; ++b) {
+#pragma unroll
+        for (int u = 0; u < AX_D; ++u) {
+            const int s = b * AX_D + u;
+            const int ub = (u - lag + 2 * AX_D) % AX_D;  // ring / meta chunk slot of chunk s - lag
+            const uint32_t pk = vopaque(mB);
+            const uint32_t lo = pk & 0xffu, hi = (pk >> 8) & 0xffu;
+            const uint32_t len_v = lo + hi + 1;
+            const uint32_t slotQs = (uint32_t)(ub * AS_SEG) * Qs + wv * Qs;
+            mB = *reinterpret_cast<const uint32_t*>(mbase + ((ub + 1) % AX_MC) * mstep);
+            const int sb = s - lag;
+            if (sb >= 0 && sb < nch) {
+                if (o_cc * AS_SEG + w < S.n) {
+                    f32x4 acc;
+                    if (FUSED) {
+                        const int len = (int)__builtin_amdgcn_readfirstlane(len_v);
+                        acc = window(r2b, wstart(slotQs, lo, span2), len_v, len, span2);
+                    } else {
+                        acc = *reinterpret_cast<const f32x4*>(r2b + slotQs);
+                    }
+#ifdef TSM_EXP_AGG_NOSTORE
+                    if (vl && acc.x == -1.f) *reinterpret_cast<f32x4*>(volq + o_off + 4 * lane) = acc;  // timing only
+#else
+                    if (vl) *reinterpret_cast<f32x4*>(volq + o_off + 4 * lane) = acc;
+#endif
+                }
+                if (++o_cc == S.cpl) {
+                    o_cc = 0;
+                    ++o_l;
+                    if (o_l < my_lines) o_off = line_base(o_l) + (size_t)w * es;
+                } else {
+                    o_off += (size_t)AS_SEG * es;
+                }
+            }
+            barrier();
+        }
+    }
+}
+
 static size_t agg_split_lds(const DevParams& P) {
     const int Q = P.Lp / 4;
     return ((size_t)AS_RP1 + AS_RP2 + 2 * AX_MIR) * Q * 16 + (size_t)AX_MC * AS_SEG * AX_MW * 4;
@@ -1276,8 +1542,10 @@ int launch_agg_stream(float* vol, const uint32_t* arms, const int32_t* ws, const
     S.rcp = reinterpret_cast<const float*>(ws_base + (size_t)(4 + horizontal) * P.H * P.W);
     S.pk = reinterpret_cast<const uint32_t*>(ws_base + (size_t)(8 + horizontal) * P.H * P.W);
     S.qtot = Q;
-    S.qn0 = Q > 64 ? (Q + 1) / 2 : Q;  // past 64 label vectors: two slices (blockIdx.y)
-    const int nslice = Q > 64 ? 2 : 1;
+    // past 64 label vectors: two slices (blockIdx.y); TSM_AGG_SLICES=2 forces two (A/B)
+    static const int force_slices = [] { const char* e = getenv("TSM_AGG_SLICES"); return e ? atoi(e) : 0; }();
+    const int nslice = (Q > 64 || force_slices == 2) ? 2 : 1;
+    S.qn0 = nslice == 2 ? (Q + 1) / 2 : Q;
     S.horizontal = horizontal;
     S.n = horizontal ? P.W : P.H;
     S.cpl = (S.n + AS_SEG - 1) / AS_SEG;
@@ -1294,8 +1562,31 @@ int launch_agg_stream(float* vol, const uint32_t* arms, const int32_t* ws, const
     // TSM_AGG_KERNEL=stream forces v5 where it fits, =split v6 for both.
     static const int pick = [] {
         const char* e = getenv("TSM_AGG_KERNEL");
-        return !e ? 0 : (e[0] == 's' && e[1] == 't') ? 1 : (e[0] == 's' && e[1] == 'p') ? 2 : 0;
+        return !e ? 0 : (e[0] == 's' && e[1] == 't') ? 1 : (e[0] == 's' && e[1] == 'p') ? 2 : (e[0] == 'v' && e[1] == '7') ? 3 : 0;
     }();
+    if (pick == 3 && !big) {  // v7: the scalar-lean role split (same LDS geometry as v6)
+        const int qs = S.qn0;
+        const size_t slds = ((size_t)AS_RP1 + AS_RP2 + 2 * AX_MIR) * qs * 16 + (size_t)AX_MC * AS_SEG * AX_MW * 4;
+        if (slds <= 160 * 1024) {
+            const dim3 sgrid(G, nslice, P.npairs);
+            const bool div = ws != nullptr;
+            auto go = [&](auto kern) {
+                static bool attr = false;  // per instantiation
+                (void)attr;
+                (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+                hipLaunchKernelGGL(kern, sgrid, dim3(AX_THREADS), slds, st, S, P);
+            };
+            if (Q == 49 && nslice == 1) {
+                if (fused) div ? go(k_agg_v7<true, true, 49>) : go(k_agg_v7<true, false, 49>);
+                else div ? go(k_agg_v7<false, true, 49>) : go(k_agg_v7<false, false, 49>);
+            } else {
+                if (fused) div ? go(k_agg_v7<true, true, 0>) : go(k_agg_v7<true, false, 0>);
+                else div ? go(k_agg_v7<false, true, 0>) : go(k_agg_v7<false, false, 0>);
+            }
+            trace_point(fused ? "k_agg_v7<fused>" : "k_agg_v7", st);
+            return 0;
+        }
+    }
     const bool v5_fits = Q <= 64 && !big && agg_stream_lds(P, fused) <= 160 * 1024;
     const bool split = pick == 2 || (pick == 0 && fused) || !v5_fits;
     if (split) {
@@ -1306,11 +1597,11 @@ int launch_agg_stream(float* vol, const uint32_t* arms, const int32_t* ws, const
         const dim3 sgrid(G, nslice, P.npairs);
         if (fused) {
             if (big) launch_split_t<true, 0, true>(S, P, sgrid, slds, st);
-            else if (Q == 49) launch_split_t<true, 49, false>(S, P, sgrid, slds, st);
+            else if (Q == 49 && nslice == 1) launch_split_t<true, 49, false>(S, P, sgrid, slds, st);
             else launch_split_t<true, 0, false>(S, P, sgrid, slds, st);
         } else {
             if (big) launch_split_t<false, 0, true>(S, P, sgrid, slds, st);
-            else if (Q == 49) launch_split_t<false, 49, false>(S, P, sgrid, slds, st);
+            else if (Q == 49 && nslice == 1) launch_split_t<false, 49, false>(S, P, sgrid, slds, st);
             else launch_split_t<false, 0, false>(S, P, sgrid, slds, st);
         }
         trace_point(fused ? "k_agg_split<fused>" : "k_agg_split", st);

@@ -274,7 +274,10 @@ __device__ __forceinline__ void partial_opt(f32x4 (&p)[J], const f32x4 (&q)[J], 
 #ifndef TSM_SC_KH
 #define TSM_SC_KH 16
 #endif
-template <bool HORIZ> constexpr int sc_k() { return HORIZ ? TSM_SC_KH : 8; }
+#ifndef TSM_SC_KV
+#define TSM_SC_KV 8
+#endif
+template <bool HORIZ> constexpr int sc_k() { return HORIZ ? TSM_SC_KH : TSM_SC_KV; }
 
 // first iteration of omp-static chunk t (libgomp / vcomp: first n%T threads take q+1)
 __device__ __forceinline__ int omp_start(int t, int n, int T) {

@@ -54,7 +54,7 @@ struct DevParams {
 
 // Largest group a launch carries (pointer tables of per-pair user buffers are kernel
 // arguments of this many entries).
-constexpr int kMaxGroup = 16;
+constexpr int kMaxGroup = 64;
 
 // Per-pair user buffers of a group (inputs, outputs), passed by value.
 struct PairIn {
