@@ -883,7 +883,7 @@ __global__ __launch_bounds__(AS_THREADS) void k_agg_stream(AggStream S, DevParam
         if (FUSED && s >= AS_LAG) {  // pass B on chunk s - LAG
             if (ob.cc * AS_SEG + wave < S.n) {
                 const f32x4 acc = window(b_off, b_len, r2_off, r2_end);
-                if (vl && (st_ok || acc.x == -1.f)) *reinterpret_cast<f32x4*>(S.vol + ob.off + 4 * lane) = acc;
+                if (vl && (st_ok || acc.x == -1.f)) st_stream(S.vol + ob.off + 4 * lane, acc);
             }
             out_step(ob);
         }
@@ -900,7 +900,7 @@ __global__ __launch_bounds__(AS_THREADS) void k_agg_stream(AggStream S, DevParam
                             *reinterpret_cast<f32x4*>(lds + r2w + (uint32_t)AS_RP2 * Qs + lane16) = acc;
                     }
                 } else if (vl && (st_ok || acc.x == -1.f)) {
-                    *reinterpret_cast<f32x4*>(S.vol + oa.off + 4 * lane) = acc;
+                    st_stream(S.vol + oa.off + 4 * lane, acc);
                 }
             }
             out_step(oa);
@@ -930,6 +930,9 @@ __global__ __launch_bounds__(AS_THREADS) void k_agg_stream(AggStream S, DevParam
 //   B waves (8): pass B of chunk s - LAG over ring2 (FUSED), or the copy of pass A's
 //     chunk s - 1 out of ring2 (single pass), and the stores to HBM.
 // One barrier per step; every wave runs the same whole number of AX_D-step blocks.
+#ifndef TSM_AGG_LDAUX
+#define TSM_AGG_LDAUX 0  // cache-policy bits of the staging loads (experiments: 2 = nt)
+#endif
 constexpr int AX_THREADS = 16 * 64;
 constexpr int AX_MW = 2;  // meta words per pixel: packed descriptor (lo, hi, size), RN(1/size)
 constexpr int AX_D = 12;  // A-wave staging ring: steps in flight (AX_D * 8 px * Q * 16 B per CU)
@@ -1103,7 +1106,7 @@ __global__ __launch_bounds__(AX_THREADS) void k_agg_split(AggStream S, DevParams
             if (BIG)
                 rv[k] = *reinterpret_cast<const f32x4*>(ivp + (size_t)pos * es + 4 * lanec);
             else
-                rv[k] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rs_vol, voff, iv + pos * es4, 0));
+                rv[k] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rs_vol, voff, iv + pos * es4, TSM_AGG_LDAUX));
 #endif
             rma[k] = (uint32_t)__builtin_amdgcn_raw_buffer_load_b32(rs_pk, vzero, ia + pos * aes4, 0);
             rmy[k] = S.ws ? (uint32_t)__builtin_amdgcn_raw_buffer_load_b32(rs_rcp, vzero, ia + pos * aes4, 0) : vzero;
@@ -1221,7 +1224,7 @@ __global__ __launch_bounds__(AX_THREADS) void k_agg_split(AggStream S, DevParams
 #ifdef TSM_EXP_AGG_NOSTORE
                     if (vl && acc.x == -1.f) *reinterpret_cast<f32x4*>(volq + ob.off + 4 * lane) = acc;  // timing only
 #else
-                    if (vl) *reinterpret_cast<f32x4*>(volq + ob.off + 4 * lane) = acc;
+                    if (vl) st_stream(volq + ob.off + 4 * lane, acc);
 #endif
                 }
                 out_step(ob);
@@ -1486,7 +1489,7 @@ __global__ __launch_bounds__(AX_THREADS) void k_agg_v7(AggStream S, DevParams Pk
 #ifdef TSM_EXP_AGG_NOSTORE
                     if (vl && acc.x == -1.f) *reinterpret_cast<f32x4*>(volq + o_off + 4 * lane) = acc;  // timing only
 #else
-                    if (vl) *reinterpret_cast<f32x4*>(volq + o_off + 4 * lane) = acc;
+                    if (vl) st_stream(volq + o_off + 4 * lane, acc);
 #endif
                 }
                 if (++o_cc == S.cpl) {

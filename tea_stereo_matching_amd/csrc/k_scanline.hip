@@ -414,7 +414,7 @@ __global__ __launch_bounds__(256) void k_scan_line(float* __restrict__ vol,
 #ifdef TSM_EXP_SCAN_NOSTORE
                         if (q[j].x == -7.f)  // timing experiment only
 #endif
-                        *reinterpret_cast<f32x4*>(cur[j]) = q[j];
+                        st_stream(cur[j], q[j]);
                 }
 #pragma unroll
                 for (int j = 0; j < J; ++j) cur[j] += dstep[j];
