@@ -477,7 +477,7 @@ __global__ __launch_bounds__(CW_THREADS) __attribute__((amdgpu_waves_per_eu(E ==
                 o3.a = c[0];
                 o3.b = c[1];
                 o3.c = c[2];
-                *reinterpret_cast<F3*>(orow + (size_t)j * Lp) = o3;
+                *reinterpret_cast<F3*>(orow + (size_t)j * Lp) = o3;  // (nt dwordx3: 206 -> 284 us)
             }
             if constexpr (E == 5) {  // labels 5l .. 5l+4: 20 B per lane, 1280 B a pixel
                 F5 o5;
@@ -491,8 +491,7 @@ __global__ __launch_bounds__(CW_THREADS) __attribute__((amdgpu_waves_per_eu(E ==
 #pragma unroll
             for (int q = 0; q < E / 4; ++q)
                 if (E * lane + 4 * q < Lp)
-                    *reinterpret_cast<f32x4*>(orow + (size_t)j * Lp + 4 * q) =
-                        f32x4{c[4 * q], c[4 * q + 1], c[4 * q + 2], c[4 * q + 3]};
+                    st_stream(orow + (size_t)j * Lp + 4 * q, f32x4{c[4 * q], c[4 * q + 1], c[4 * q + 2], c[4 * q + 3]});
         }
         if constexpr (SHEAR) {
             // delay line by step rotation (compile-time slots): element e of the float4
@@ -588,8 +587,7 @@ __global__ __launch_bounds__(CW_THREADS) __attribute__((amdgpu_waves_per_eu(E ==
                     c4[t] = (fixed_ok && k >= klo && k <= khi) ? c : 2.f;
                 }
             }
-            *reinterpret_cast<f32x4*>(vol + (((size_t)v * H + y) * W + j) * Lp + 64 * E) =
-                f32x4{c4[0], c4[1], c4[2], c4[3]};
+            st_stream(vol + (((size_t)v * H + y) * W + j) * Lp + 64 * E, f32x4{c4[0], c4[1], c4[2], c4[3]});
         }
     }
     CW_STAMP(3);

@@ -191,7 +191,7 @@ __device__ __forceinline__ void scan_issue(StepIn<J>& s, int pos, int dir, int l
                                            const ScanConst& C) {
     const int pm = dir > 0 ? pos : pos + 1;  // max(pos, predecessor)
 #pragma unroll
-    for (int j = 0; j < J; ++j) s.p[j] = *reinterpret_cast<const f32x4*>(pv[j]);
+    for (int j = 0; j < J; ++j) s.p[j] = *reinterpret_cast<const f32x4*>(pv[j]);  // (nt loads: -2 %)
     const uint32_t i1 = (uint32_t)(HORIZ ? C.gpad + pm : pm * C.gstride + C.gpad + line);
     s.d1 = (int)__builtin_amdgcn_raw_buffer_load_b8(R.own, 0u, orow + i1, 0);
     s.mk = 1u;
