@@ -268,11 +268,12 @@ __device__ __forceinline__ void partial_opt(f32x4 (&p)[J], const f32x4 (&q)[J], 
 // omp schedule emulation costs two scalar compares per step (chunk starts are tracked
 // incrementally).
 // ---------------------------------------------------------------------------
-// Prefetch depth (steps).  The vertical passes run ~2.4 waves per SIMD over strided
-// columns and are HBM-bound at 8; the horizontal ones have under one wave per SIMD, so
-// each wave must keep more of its own row in flight.
+// Prefetch depth (steps).  Alone, a pass of the horizontal kernel (under one wave per
+// SIMD) is faster with 16 steps in flight; in groups of 32 pairs (24000 waves a launch)
+// 8 steps win (+1 % pairs/s, same-box A/B): 79 instead of 135 VGPRs, 6 instead of 3
+// waves per SIMD.  The vertical passes are HBM-bound at 8.
 #ifndef TSM_SC_KH
-#define TSM_SC_KH 16
+#define TSM_SC_KH 8
 #endif
 #ifndef TSM_SC_KV
 #define TSM_SC_KV 8
