@@ -375,6 +375,188 @@ __global__ __launch_bounds__(VD_THREADS) void k_vote_decide(
 }
 
 // ---------------------------------------------------------------------------
+// region voting, outlier-list form (the default)
+// ---------------------------------------------------------------------------
+// The outliers (disp < minD) are ranked in raster order first (one block scan), so the
+// vote count runs on them alone, 16 lanes an outlier, and writes its vote and (for a
+// low-vote outlier) its samples straight in rank order; the decision walks, for each
+// high-vote outlier, its region and then the low-vote outliers ranked just before it back
+// to the previous high-vote one: exactly the histogram the reference carries in raster
+// order (:1132-1151).  No per-pixel vote / sample / flag maps and no second scan.
+__global__ void k_oscan_count(const int32_t* __restrict__ disp, int n, int minD, int32_t* __restrict__ bsum,
+                              size_t ps) {
+    pair_shift(blockIdx.z, ps, disp, bsum);
+    __shared__ int sa[SC_THREADS], sb[SC_THREADS];
+    const int base = blockIdx.x * SC_BLOCK + threadIdx.x * SC_ITEMS;
+    int a = 0, b = 0;
+    for (int k = 0; k < SC_ITEMS; ++k) {
+        const int p = base + k;
+        if (p < n && disp[p] < minD) a++;
+    }
+    block_scan2(a, b, sa, sb);
+    if (threadIdx.x == SC_THREADS - 1) {
+        bsum[2 * blockIdx.x] = sa[SC_THREADS - 1];
+        bsum[2 * blockIdx.x + 1] = 0;
+    }
+}
+
+// out_list[rank] = pixel of each outlier; dtmp = disp everywhere (the Jacobi output
+// starts as the input; the decision overwrites high-vote outliers)
+__global__ void k_oscan_scatter(const int32_t* __restrict__ disp, int n, int minD, const int32_t* __restrict__ bsum,
+                                int32_t* __restrict__ out_list, int32_t* __restrict__ dtmp, size_t ps) {
+    pair_shift(blockIdx.z, ps, disp, bsum, out_list, dtmp);
+    __shared__ int sa[SC_THREADS], sb[SC_THREADS];
+    const int base = blockIdx.x * SC_BLOCK + threadIdx.x * SC_ITEMS;
+    int a = 0, b = 0;
+    for (int k = 0; k < SC_ITEMS; ++k) {
+        const int p = base + k;
+        if (p < n && disp[p] < minD) a++;
+    }
+    block_scan2(a, b, sa, sb);
+    a += bsum[2 * blockIdx.x];
+    for (int k = 0; k < SC_ITEMS; ++k) {
+        const int p = base + k;
+        if (p >= n) break;
+        const int d = disp[p];
+        dtmp[p] = d;
+        if (d < minD) out_list[a++] = p;
+    }
+}
+
+// Vote count of every ranked outlier, 16 lanes an outlier (4 a wave), grid-stride over
+// ranks; lanes take every 16th outer-arm position and a low-vote outlier (every valid
+// sample kept) walks its region again to place its samples at the lanes' prefix slots.
+__global__ __launch_bounds__(256) void k_vote_count_rank(const int32_t* __restrict__ disp,
+                                                         const uint32_t* __restrict__ arms,
+                                                         const int32_t* __restrict__ out_list,
+                                                         const int32_t* __restrict__ counts,
+                                                         int32_t* __restrict__ cvote, uint16_t* __restrict__ csamp,
+                                                         int hf, DevParams Pk) {
+    const DevParams P = Pk;
+    pair_shift(blockIdx.z, P.pstride, disp, arms, out_list, counts, cvote, csamp);
+    const int lane = threadIdx.x & 63, sub = lane & 15, base = lane & ~15;
+    const int W = P.W, minD = P.minD;
+    const int nout = counts[0];
+    const int ngroups = (gridDim.x * blockDim.x) >> 4;
+    // every group of a wave runs the same number of iterations (shuffles stay in step)
+    const int g0 = (blockIdx.x * blockDim.x + threadIdx.x) >> 4;
+    const int wave_g0 = g0 & ~3;
+    for (int it = wave_g0; it < nout; it += ngroups) {
+        const int a = it + (g0 & 3);
+        const bool valid = a < nout;
+        const int p = valid ? out_list[a] : 0;
+        const int y = p / W, x = p - y * W;
+        int oA = 0, oB = -1, iA, iB;
+        if (valid) region_arms(arms[p], hf, oA, oB, iA, iB);
+        auto walk = [&](bool emit, int pos, uint16_t* smp) {
+            int cnt = 0;
+            for (int o = -oA + sub; o <= oB; o += 16) {
+                const int yy0 = hf ? y + o : y, xx0 = hf ? x : x + o;
+                int a1, b1, a2, b2;
+                region_arms(arms[(size_t)yy0 * W + xx0], hf, a1, b1, a2, b2);
+                const ptrdiff_t st = hf ? 1 : W;
+                const int32_t* rp = disp + (size_t)yy0 * W + xx0;
+                for (int i = -a2; i <= b2; ++i) {
+                    const int dv = rp[(ptrdiff_t)i * st];
+                    if (dv >= minD) {
+                        if (emit) smp[pos + cnt] = (uint16_t)(dv - minD);
+                        cnt++;
+                    }
+                }
+            }
+            return cnt;
+        };
+        const int mine = walk(false, 0, nullptr);
+        int incl = mine;
+#pragma unroll
+        for (int d = 1; d < 16; d <<= 1) {
+            const int v = __shfl_up(incl, d, 16);
+            if (sub >= d) incl += v;
+        }
+        const int total = __shfl(incl, base + 15);
+        if (valid && total <= kMaxSamples && mine > 0) walk(true, incl - mine, csamp + (size_t)a * kMaxSamples);
+        if (valid && sub == 0) cvote[a] = total;
+    }
+}
+
+// One wave per high-vote ranked outlier (grid-stride): LDS histogram of its own region,
+// plus the samples of the low-vote outliers ranked between the previous high-vote one
+// and it, then the first argmax and the ratio test (:1137-1153).
+__global__ __launch_bounds__(VD_THREADS) void k_vote_decide_rank(
+    const int32_t* __restrict__ disp, int32_t* __restrict__ dtmp, const uint32_t* __restrict__ arms,
+    const int32_t* __restrict__ out_list, const int32_t* __restrict__ cvote, const uint16_t* __restrict__ csamp,
+    const int32_t* __restrict__ counts, int hf, DevParams Pk) {
+    const DevParams P = Pk;
+    pair_shift(blockIdx.z, P.pstride, disp, dtmp, arms, out_list, cvote, csamp, counts);
+    extern __shared__ int hist_all[];
+    const int L = P.L, W = P.W, minD = P.minD, thr = P.voting_thresh;
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    int* hist = hist_all + wave * L;
+    const int nout = counts[0];
+    const int nwaves = gridDim.x * (VD_THREADS / 64);
+    for (int r = blockIdx.x * (VD_THREADS / 64) + wave; r < nout; r += nwaves) {
+        const int v = cvote[r];
+        if (v <= thr) continue;  // low vote: the pixel keeps its value (dtmp holds it)
+        for (int d = lane; d < L; d += 64) hist[d] = 0;
+        __builtin_amdgcn_wave_barrier();
+        const int p = out_list[r];
+        const int y = p / W, x = p - y * W;
+        int oA, oB, iA, iB;
+        region_arms(arms[p], hf, oA, oB, iA, iB);
+        for (int o = -oA + lane; o <= oB; o += 64) {
+            const int yy0 = hf ? y + o : y, xx0 = hf ? x : x + o;
+            int a1, b1, a2, b2;
+            region_arms(arms[(size_t)yy0 * W + xx0], hf, a1, b1, a2, b2);
+            const ptrdiff_t st = hf ? 1 : W;
+            const int32_t* rp = disp + (size_t)yy0 * W + xx0;
+            int i = -a2;
+            for (; i + 3 <= b2; i += 4) {
+                const int d0 = rp[(ptrdiff_t)i * st], d1 = rp[(ptrdiff_t)(i + 1) * st];
+                const int d2 = rp[(ptrdiff_t)(i + 2) * st], d3 = rp[(ptrdiff_t)(i + 3) * st];
+                if (d0 >= minD) atomicAdd(&hist[d0 - minD], 1);
+                if (d1 >= minD) atomicAdd(&hist[d1 - minD], 1);
+                if (d2 >= minD) atomicAdd(&hist[d2 - minD], 1);
+                if (d3 >= minD) atomicAdd(&hist[d3 - minD], 1);
+            }
+            for (; i <= b2; ++i) {
+                const int dv = rp[(ptrdiff_t)i * st];
+                if (dv >= minD) atomicAdd(&hist[dv - minD], 1);
+            }
+        }
+        // carried: ranks r-1, r-2, ... down to (not including) the previous high-vote one
+        for (int top = r - 1; top >= 0; top -= 64) {
+            const int k = top - lane;
+            const int ck = k >= 0 ? cvote[k] : 0;
+            const uint64_t him = __ballot(k >= 0 && ck > thr);
+            const int stop = him ? (int)__builtin_ctzll(him) : 64;  // first high-vote lane (nearest r)
+            if (k >= 0 && lane < stop) {
+                const uint32_t* s = reinterpret_cast<const uint32_t*>(csamp + (size_t)k * kMaxSamples);
+                uint32_t wv[kMaxSamples / 2];
+#pragma unroll
+                for (int i = 0; i < kMaxSamples / 2; ++i) wv[i] = s[i];
+#pragma unroll
+                for (int m = 0; m < kMaxSamples; ++m)
+                    if (m < ck) atomicAdd(&hist[(wv[m >> 1] >> (16 * (m & 1))) & 0xffffu], 1);
+            }
+            if (him) break;
+        }
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+        uint64_t best = ~0ull;
+        for (int d = lane; d < L; d += 64) {
+            const uint64_t key = ((uint64_t)(0xffffffffu - (uint32_t)hist[d]) << 32) | (uint32_t)d;
+            best = key < best ? key : best;
+        }
+        best = wave_min_u64(best);
+        const int cmax = (int)(0xffffffffu - (uint32_t)(best >> 32));
+        const int dbest = (int)(uint32_t)best;
+        const float ratio = cmax / (float)v;
+        if (lane == 0) dtmp[p] = ratio > P.voting_ratio && cmax > 0 ? dbest + minD : disp[p];
+        __builtin_amdgcn_wave_barrier();
+    }
+}
+
+// ---------------------------------------------------------------------------
 // proper interpolation
 // ---------------------------------------------------------------------------
 // 16 rays of (:1166-1167); the reference steps d/2 then d - d/2 (C++ truncating /2).
@@ -907,6 +1089,31 @@ void launch_region_voting(RefineBufs& B, const uint32_t* arms0, int hf, const De
     const int n = P.H * P.W;
     const int nb = (int)refine_scan_blocks(n);
     const size_t ps = P.pstride;
+    static const bool old_flow = [] {
+        const char* e = getenv("TSM_VOTE_FLOW");  // A/B: "old" = the per-pixel count + two-counter scan
+        return e && e[0] == 'o';
+    }();
+    if (!old_flow) {
+        hipLaunchKernelGGL(k_oscan_count, grid1d(nb, P), dim3(SC_THREADS), 0, st, B.dm, n, P.minD, B.bsum, ps);
+        trace_point("k_oscan_count", st);
+        hipLaunchKernelGGL(k_scan_blocks, grid1d(1, P), dim3(SC_THREADS), 0, st, B.bsum, nb, B.counts, ps);
+        trace_point("k_scan_blocks", st);
+        hipLaunchKernelGGL(k_oscan_scatter, grid1d(nb, P), dim3(SC_THREADS), 0, st, B.dm, n, P.minD, B.bsum,
+                           B.out_list, B.dtmp, ps);
+        trace_point("k_oscan_scatter", st);
+        // grid-stride over the ranked outliers (their count stays on the device)
+        const int vc_blocks = std::max(64, 1536 / std::max(1, P.npairs));
+        hipLaunchKernelGGL(k_vote_count_rank, grid1d(vc_blocks, P), dim3(256), 0, st, B.dm, arms0, B.out_list,
+                           B.counts, B.cvote, B.csamp, hf, P);
+        trace_point("k_vote_count_rank", st);
+        const size_t lds = (size_t)(VD_THREADS / 64) * P.L * sizeof(int);
+        const int vd_blocks = std::max(128, 1024 / std::max(1, P.npairs));
+        hipLaunchKernelGGL(k_vote_decide_rank, grid1d(vd_blocks, P), dim3(VD_THREADS), lds, st, B.dm, B.dtmp,
+                           arms0, B.out_list, B.cvote, B.csamp, B.counts, hf, P);
+        trace_point("k_vote_decide_rank", st);
+        std::swap(B.dm, B.dtmp);
+        return;
+    }
     static const bool serial = [] {
         const char* e = getenv("TSM_VOTE_SERIAL");  // A/B: the one-thread-per-pixel count
         return e && e[0] == '1';
