@@ -594,6 +594,317 @@ __global__ __launch_bounds__(CW_THREADS) __attribute__((amdgpu_waves_per_eu(E ==
 }
 
 // ---------------------------------------------------------------------------
+// cost-volume build on the matrix cores (RGB, no mask): the census term as an fp4 MFMA
+// ---------------------------------------------------------------------------
+// The census count of a (fixed, varying) record pair is a dot product over the 384 bits
+// of 12 words: census = sum_w popc(F[w] & V[(w + 6) % 12]) (gt planes against lt planes
+// and back).  Expanding every bit to an fp4 (e2m1) element -- 2.0 where set, 0 where not --
+// makes one 16x16x128 block-scaled MFMA (scales 1.0) sum 4 x the matches of 128 bits for a
+// 16 x 16 tile of (fixed pixel j, varying pixel x) pairs, exactly (integers <= 1536 in
+// f32), and three of them give 4 x census: the byte offset of the census table entry.
+// Lane l of MFMA kk carries word 4 kk + (l >> 4) of row / column l & 15, expanded so that
+// bit 4n + s of the word lands in nibble n of dword s: both operands place every bit at
+// the same k, which is all a dot product needs (tools/micro/fp4_census_dot.hip checks it
+// on the device).  The AD term and the two tables stay on the VALU / LDS: per cell one
+// v_sad_u8, two table reads, one subtraction -- against 6 x (and, and_or, bcnt) + the
+// shift-register DPP moves of the walk.
+//
+// A workgroup (8 waves) owns a unit (view, row, 128-pixel segment); wave w owns the 16
+// pixels j0 = seg + 16 w.  Pixel j's labels k = 0..L-1 pair it with x = j - k (view 0)
+// or j + k (view 1), so the wave's tiles are the x-blocks x0 = j0 -+ 16 m, m = 0..M with
+// M = ceil((L - 1) / 16).  The unit's varying records (128 + 16 M pixels) are expanded
+// once into LDS as B fragments, [word][pixel] 16 B each (a tile's 64 lanes read 16
+// consecutive pixels per word: conflict-free ds_read_b128); the fixed records become
+// the wave's A fragments in registers.  Output lane l of a tile holds x = x0 + (l & 15)
+// and j = j0 + 4 (l >> 4) + r (C/D map col = lane & 15, row = 4 (lane >> 4) + reg), so one
+// store per r writes 16 consecutive labels of 4 pixels (64-B runs, descending k).
+// Cells: same formula and borders as k_cost_walk (costInitialize :542-579):
+// c = (2 - A[ad]) - B[census] where the fixed pixel's and the varying pixel's windows
+// are inside the image, 2 elsewhere, +inf on the padding labels L..Lp-1.
+constexpr int CM_WAVES = 8;
+constexpr int CM_THREADS = CM_WAVES * 64;
+constexpr int CM_JB = 16;                   // pixels per wave (one tile row block)
+constexpr int CM_SEG = CM_WAVES * CM_JB;    // pixels per unit
+constexpr uint32_t CM_BIAS = 64;            // store buffer starts this many bytes before the row
+
+typedef int v8i_ __attribute__((ext_vector_type(8)));
+typedef float v4f_ __attribute__((ext_vector_type(4)));
+
+// 32 census bits -> 32 fp4 elements (16 B): bit 4n + s -> nibble n of dword s, 0x4 = 2.0
+__device__ __forceinline__ u32x4 fp4_expand(uint32_t w) {
+    return u32x4{(w << 2) & 0x44444444u, (w << 1) & 0x44444444u, w & 0x44444444u, (w >> 1) & 0x44444444u};
+}
+
+__device__ __forceinline__ v4f_ mfma_fp4(u32x4 a, u32x4 b, v4f_ c) {
+    const v8i_ av = {(int)a.x, (int)a.y, (int)a.z, (int)a.w, 0, 0, 0, 0};
+    const v8i_ bv = {(int)b.x, (int)b.y, (int)b.z, (int)b.w, 0, 0, 0, 0};
+    // cbsz = blgp = 4: both operands fp4 (e2m1); E8M0 scales 127 = 1.0
+    return __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(av, bv, c, 4, 4, 0, 127, 0, 127);
+}
+
+__host__ __device__ inline int cost_mfma_tiles(int L) { return (L - 1 + CM_JB - 1) / CM_JB; }  // M
+__host__ __device__ inline int cost_mfma_span(int L) { return CM_SEG + CM_JB * cost_mfma_tiles(L); }
+
+// MT > 0: the tile count M at compile time (LDS offsets become immediates); 0: runtime
+template <int MT>
+__global__ __launch_bounds__(CM_THREADS) __attribute__((amdgpu_waves_per_eu(4))) void k_cost_mfma(const uint32_t* __restrict__ desc,
+                                                          const float* __restrict__ lutA, int lutA_n,
+                                                          const float* __restrict__ lutB,
+                                                          float* __restrict__ vol, DevParams Pk, int nseg) {
+    const DevParams P = Pk;
+    __shared__ float sA2[768];  // 2 - A[ad]
+    __shared__ float sB[192];   // B[census]
+    extern __shared__ __attribute__((aligned(16))) u32x4 smem_frag[];
+    const int H = P.H, W = P.W, L = P.L, Lp = P.Lp;
+    const int M = MT > 0 ? MT : cost_mfma_tiles(L), XS = CM_SEG + CM_JB * M;
+    u32x4* xfr = smem_frag;                                       // [12][XS]
+    uint32_t* xcol = reinterpret_cast<uint32_t*>(smem_frag + 12 * XS);  // [XS]
+    pair_shift(blockIdx.z, P.pstride, desc, vol);
+    // XCD-aware unit order (as k_cost_walk): each XCD takes a contiguous run of units, so
+    // the segments and both views of a row share one L2 for their records
+    const int nb = gridDim.x, per = nb >> 3;
+    const int blk = (int)blockIdx.x < 8 * per ? ((int)blockIdx.x & 7) * per + ((int)blockIdx.x >> 3) : (int)blockIdx.x;
+    if (blk >= 2 * H * nseg) return;  // whole workgroup: no barrier is pending
+    const int seg = blk % nseg, vy = blk / nseg;
+    const int v = vy & 1, y = vy >> 1;
+    const int seg_lo = seg * CM_SEG;
+    const int xs0 = v == 0 ? seg_lo - CM_JB * M : seg_lo;  // first staged varying pixel
+    const int hw = P.censusW >> 1, hh = P.censusH >> 1;
+    const bool rowOut = y - hh < 0 || y + hh >= H;
+    const int foff = v == 0 ? -P.minD : P.minD;
+    const uint32_t* dF = desc + ((size_t)v * H + y) * W * 16;        // fixed image row
+    const uint32_t* dV = desc + ((size_t)(1 - v) * H + y) * W * 16;  // varying image row
+
+    for (int i = threadIdx.x; i < lutA_n && i < 768; i += CM_THREADS) sA2[i] = 2.f - lutA[i];
+    for (int i = threadIdx.x; i < 192; i += CM_THREADS) sB[i] = i < 188 ? lutB[i] : 0.f;
+    // stage the varying records as B fragments: word slot s holds V word (s + 6) % 12
+    for (int p = threadIdx.x; p < XS; p += CM_THREADS) {
+        const int x = xs0 + p;
+        u32x4 r0 = {0u, 0u, 0u, 0u}, r1 = r0, r2 = r0, r3 = r0;
+        if (x >= 0 && x < W) {
+            const u32x4* r = reinterpret_cast<const u32x4*>(dV + (size_t)x * 16);
+            r0 = r[0]; r1 = r[1]; r2 = r[2]; r3 = r[3];
+        }
+        const uint32_t w[12] = {r0.x, r0.y, r0.z, r0.w, r1.x, r1.y, r1.z, r1.w, r2.x, r2.y, r2.z, r2.w};
+#pragma unroll
+        for (int s = 0; s < 12; ++s) xfr[s * XS + p] = fp4_expand(w[(s + 6) % 12]);
+        xcol[p] = r3.x;
+    }
+    __syncthreads();
+
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
+    const int j0 = seg_lo + CM_JB * wave;
+    if (j0 >= W) return;
+    const int col = lane & 15, grp = lane >> 4;
+    auto clampx = [&](int x) { return x < 0 ? 0 : (x >= W ? W - 1 : x); };
+    // A fragments: row j0 + col, words 4 kk + grp of its fixed record
+    u32x4 af[3];
+    {
+        const uint32_t* rf = dF + (size_t)clampx(j0 + col + foff) * 16;
+#pragma unroll
+        for (int kk = 0; kk < 3; ++kk) af[kk] = fp4_expand(rf[4 * kk + grp]);
+    }
+    // this lane's four output rows j = j0 + 4 grp + r: fixed colour and window test
+    uint32_t fc[4];
+    bool fo[4];
+    bool rows_in = j0 + CM_JB <= W;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+        const int j = j0 + 4 * grp + r;
+        const int xf = j + foff;
+        fc[r] = dF[(size_t)clampx(xf) * 16 + 12];
+        fo[r] = !rowOut && xf - hw >= 0 && xf + hw < W;
+        rows_in = rows_in && fo[r];
+    }
+    rows_in = __all(rows_in);  // every row of the block inside the image with its window
+    // cell (r, m): label k = kb + ks r + 16 m at byte ob[r] + 64 m of the row's volume
+    const int kb = v == 0 ? 4 * grp - col : col - 4 * grp;
+    const int ks = v == 0 ? 1 : -1;
+    uint32_t ob[4];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) ob[r] = CM_BIAS + 4u * (uint32_t)((j0 + 4 * grp + r) * Lp + kb + ks * r);
+    // fast tiles store quad-transposed float4s: pixel j0 + 4 grp + (col & 3), labels from
+    // kq (m = 0) on, kq = 4 grp + i - 4 q - 3 (view 0) or 4 q - 4 grp - i (view 1)
+    uint32_t oq;
+    {
+        const int i = col & 3, q4 = col & ~3;
+        const int kq = v == 0 ? 4 * grp + i - q4 - 3 : q4 - 4 * grp - i;
+        oq = CM_BIAS + 4u * (uint32_t)((j0 + 4 * grp + i) * Lp + kq);
+    }
+#ifdef TSM_EXP_CM_ALIGNED  // timing only: each tile's 16 labels as one 64-B aligned piece
+#pragma unroll
+    for (int r = 0; r < 4; ++r) ob[r] = CM_BIAS + (uint32_t)(j0 + 4 * grp + r) * 832u + 4u * (uint32_t)col;
+    oq = CM_BIAS + (uint32_t)(j0 + 4 * grp + (col & 3)) * 832u + 4u * (uint32_t)(col & ~3);
+#endif
+    // the row's volume as a raw buffer: a store whose VGPR offset is past the buffer's
+    // size is dropped, so cells outside the label band / image are masked without
+    // branches.  The range check covers the VGPR offset only (the tile step 64 m rides in
+    // soffset), so the buffer starts CM_BIAS bytes before the row: a valid cell's VGPR
+    // part ob[r] >= 4 (k >= -15 at m = 0) stays non-negative.
+    const uint32_t row_bytes = 4u * (uint32_t)(W * Lp);
+    const __amdgpu_buffer_rsrc_t vrs = __builtin_amdgcn_make_buffer_rsrc(
+        reinterpret_cast<char*>(vol + ((size_t)v * H + y) * W * Lp) - CM_BIAS, (short)0, (int)(row_bytes + CM_BIAS),
+        0x00020000);
+    // tile m's varying pixels start at staged pixel pb + ps m (uniform)
+    const int pb = v == 0 ? CM_JB * (wave + M) : CM_JB * wave, ps = v == 0 ? -CM_JB : CM_JB;
+    const u32x4* xl = xfr + grp * XS + col;
+    const uint32_t* cl = xcol + col;
+    // one tile: 3 MFMAs for the census, then per cell the AD term and the two tables.
+    // FAST: every cell in the label band, both windows inside the image (no selects, no
+    // masks); otherwise out-of-band / off-image cells get an offset past the buffer
+    // (the store is dropped) and cells with a window off the image cost 2.
+    auto mma = [&](int m) {
+        const int p0 = pb + ps * m;
+        v4f_ acc = {0.f, 0.f, 0.f, 0.f};
+#ifdef TSM_EXP_CM_STOREONLY
+        return acc;
+#endif
+#pragma unroll
+        for (int kk = 0; kk < 3; ++kk) acc = mfma_fp4(af[kk], xl[4 * kk * XS + p0], acc);
+        return acc;
+    };
+    // FASTc: 0 = general tile, 1 = fast tile of view 0, 2 = fast tile of view 1
+    auto epilogue = [&](int m, v4f_ acc, auto FASTc) {
+        constexpr bool FAST = decltype(FASTc)::value != 0;
+        constexpr bool FV0 = decltype(FASTc)::value == 1;
+        const int p0 = pb + ps * m;
+        const uint32_t vc = cl[p0];
+        const int mo = 64 * m;  // byte step of the tile's labels (soffset)
+        bool xok = true;
+        if (!FAST) {
+            const int x = xs0 + p0 + col;
+            xok = x - hw >= 0 && x + hw < W;
+        }
+        float c[4];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+#ifdef TSM_EXP_CM_STOREONLY  // timing only: no MFMA results, no tables
+            c[r] = (float)(m + r);
+#else
+            const uint32_t cen4 = (uint32_t)acc[r];  // 4 x census: byte offset into sB
+            const uint32_t ad4 = __builtin_amdgcn_sad_u8(fc[r], vc, 0u) << 2;
+            c[r] = *reinterpret_cast<const float*>(reinterpret_cast<const char*>(sA2) + ad4) -
+                   *reinterpret_cast<const float*>(reinterpret_cast<const char*>(sB) + cen4);
+#endif
+        }
+        if (FAST) {
+            // 4x4 transpose inside each quad of lanes (two DPP butterflies): lane 4q + i
+            // then holds pixel j0 + 4 grp + i at x = x0 + 4q + e in c[e], four consecutive
+            // labels, and leaves them with one 16-B store instead of four 4-B ones
+            const bool b1 = (col & 2) != 0, b0 = (col & 1) != 0;
+            auto qp = [](float x, auto CTc) {  // quad_perm move (every lane has a source)
+                return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(x), decltype(CTc)::value, 0xF, 0xF, true));
+            };
+            float r0 = qp(b1 ? c[0] : c[2], IC<DPP_QUAD_2301>{});
+            float r1 = qp(b1 ? c[1] : c[3], IC<DPP_QUAD_2301>{});
+            c[0] = b1 ? r0 : c[0]; c[1] = b1 ? r1 : c[1];
+            c[2] = b1 ? c[2] : r0; c[3] = b1 ? c[3] : r1;
+            r0 = qp(b0 ? c[0] : c[1], IC<DPP_QUAD_1032>{});
+            r1 = qp(b0 ? c[2] : c[3], IC<DPP_QUAD_1032>{});
+            c[0] = b0 ? r0 : c[0]; c[2] = b0 ? r1 : c[2];
+            c[1] = b0 ? c[1] : r0; c[3] = b0 ? c[3] : r1;
+            const u32x4 q = FV0 ? u32x4{__float_as_uint(c[3]), __float_as_uint(c[2]), __float_as_uint(c[1]), __float_as_uint(c[0])}
+                                   : u32x4{__float_as_uint(c[0]), __float_as_uint(c[1]), __float_as_uint(c[2]), __float_as_uint(c[3])};
+#ifdef TSM_EXP_CM_NOSTORE
+            if (c[0] == -12345.f)
+#endif
+            __builtin_amdgcn_raw_buffer_store_b128(q, vrs, (int)oq, mo, 0);
+        } else {
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const int k = kb + ks * r + CM_JB * m;
+                const float cr = (fo[r] && xok) ? c[r] : 2.f;
+                const int off = ((unsigned)k < (unsigned)L && j0 + 4 * grp + r < W) ? (int)ob[r] : -1;
+#ifdef TSM_EXP_CM_NOSTORE
+                if (cr == -12345.f)
+#endif
+                __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(cr), vrs, off, mo, 0);
+            }
+        }
+    };
+    auto tile = [&](int m, auto FASTc) { epilogue(m, mma(m), FASTc); };
+    // fast tiles: m in [1, (L - 16) / 16] (inside the label band) whose 16 varying pixels
+    // and windows are inside the image, for a block whose rows all are
+    int f_lo = 1, f_hi = (L - CM_JB) / CM_JB;
+    {
+        const int xb = xs0 + pb;  // x0(m) = xb + ps m
+        const int lo_x = hw, hi_x = W - hw - CM_JB;  // x0 in [lo_x, hi_x]
+        if (v == 0) {  // x0 = xb - 16 m
+            f_lo = max(f_lo, (xb - hi_x + CM_JB - 1) >= 0 ? (xb - hi_x + CM_JB - 1) / CM_JB : 0);
+            f_hi = min(f_hi, xb - lo_x >= 0 ? (xb - lo_x) / CM_JB : -1);
+        } else {  // x0 = xb + 16 m
+            f_lo = max(f_lo, lo_x - xb > 0 ? (lo_x - xb + CM_JB - 1) / CM_JB : 0);
+            f_hi = min(f_hi, hi_x - xb >= 0 ? (hi_x - xb) / CM_JB : -1);
+        }
+        if (!rows_in || f_hi < f_lo) { f_lo = M + 1; f_hi = M; }
+    }
+#ifdef TSM_EXP_CM_BURST
+    if constexpr (MT > 0) {
+        // experiment: all tiles first, their cells held in registers, then the block's
+        // stores in one burst (every pixel vector completed within a short window).
+        // Measured slower than streaming the stores tile by tile: 208.8 vs 198.8 us.
+        float cb[MT + 1][4];
+#pragma unroll
+        for (int m = 0; m <= MT; ++m) {
+            const v4f_ acc = mma(m);
+            const bool fast = m >= f_lo && m <= f_hi;
+            const int p0 = pb + ps * m;
+            const uint32_t vc = cl[p0];
+            const int x = xs0 + p0 + col;
+            const bool xok = fast || (x - hw >= 0 && x + hw < W);
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const uint32_t cen4 = (uint32_t)acc[r];
+                const uint32_t ad4 = __builtin_amdgcn_sad_u8(fc[r], vc, 0u) << 2;
+                const float c = *reinterpret_cast<const float*>(reinterpret_cast<const char*>(sA2) + ad4) -
+                                *reinterpret_cast<const float*>(reinterpret_cast<const char*>(sB) + cen4);
+                cb[m][r] = (fast || (fo[r] && xok)) ? c : 2.f;
+            }
+        }
+#pragma unroll
+        for (int m = 0; m <= MT; ++m) {
+            const bool fast = m >= f_lo && m <= f_hi;
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const int k = kb + ks * r + CM_JB * m;
+                const bool in = fast || ((unsigned)k < (unsigned)L && j0 + 4 * grp + r < W);
+#ifdef TSM_EXP_CM_NOSTORE
+                if (cb[m][r] == -12345.f)
+#endif
+                __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(cb[m][r]), vrs, in ? (int)ob[r] : -1, 64 * m, 0);
+            }
+        }
+    } else
+#endif
+    {
+    for (int m = 0; m < min(f_lo, M + 1); ++m) tile(m, IC<0>{});
+    // fast tiles two at a time: tile m + 1's MFMAs overlap tile m's epilogue
+    auto fast_run = [&](auto Fc) {
+        int m = f_lo;
+        for (; m < f_hi; m += 2) {
+            const v4f_ a0 = mma(m), a1 = mma(m + 1);
+            epilogue(m, a0, Fc);
+            epilogue(m + 1, a1, Fc);
+        }
+        if (m == f_hi) tile(m, Fc);
+    };
+    if (v == 0) fast_run(IC<1>{});
+    else fast_run(IC<2>{});
+    for (int m = max(f_hi + 1, min(f_lo, M + 1)); m <= M; ++m) tile(m, IC<0>{});
+    }
+    // padding labels L..Lp-1: +inf (lane = pixel)
+    if (Lp > L && lane < CM_JB && j0 + lane < W) {
+        for (int k = L; k < Lp; ++k)
+            __builtin_amdgcn_raw_buffer_store_b32(0x7f800000u, vrs, (int)(CM_BIAS + 4u * (uint32_t)((j0 + lane) * Lp + k)), 0, 0);
+    }
+}
+
+size_t cost_mfma_lds_bytes(const DevParams& P) {
+    const int XS = cost_mfma_span(P.L);
+    return (size_t)XS * 12 * 16 + (size_t)XS * 4;
+}
+
+// ---------------------------------------------------------------------------
 // launchers
 // ---------------------------------------------------------------------------
 void launch_pack(const PairIn& in, size_t step, uint32_t* img, const DevParams& P, hipStream_t st) {
@@ -717,7 +1028,32 @@ int launch_cost_volume(const uint32_t* img, const uint32_t* desc, const float* l
                        uint32_t& ctr_base, hipStream_t st) {
     (void)img;
     const bool hsi = P.color_model == 1;
-#define CASE(E)                                                                                    \
+    // RGB without mask mode: the matrix-core build (TSM_COST_MFMA=0 keeps the walk)
+    static const bool use_mfma = [] {
+        const char* e = getenv("TSM_COST_MFMA");
+        return !(e && e[0] == '0');
+    }();
+    const size_t mlds = cost_mfma_lds_bytes(P);
+    if (use_mfma && !hsi && !P.mask && lutA_n <= 768 && mlds + 4 * (768 + 192) <= 160 * 1024) {
+        static bool attr = false;
+        if (!attr) {
+            (void)hipFuncSetAttribute((const void*)k_cost_mfma<0>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                      160 * 1024 - 4 * (768 + 192));
+            (void)hipFuncSetAttribute((const void*)k_cost_mfma<12>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                      160 * 1024 - 4 * (768 + 192));
+            attr = true;
+        }
+        const int nseg = (P.W + CM_SEG - 1) / CM_SEG;
+        const int units = 2 * P.H * nseg;
+        const dim3 g((units + 7) / 8 * 8, 1, P.npairs);  // whole multiples of the 8 XCDs
+        if (cost_mfma_tiles(P.L) == 12)  // L = 178..193 (config B)
+            hipLaunchKernelGGL(k_cost_mfma<12>, g, dim3(CM_THREADS), mlds, st, desc, lutA, lutA_n, lutB, vol, P, nseg);
+        else
+            hipLaunchKernelGGL(k_cost_mfma<0>, g, dim3(CM_THREADS), mlds, st, desc, lutA, lutA_n, lutB, vol, P, nseg);
+        trace_point("k_cost_mfma", st);
+        return 0;
+    }
+#define CASE(E)                                                                                  \
     if (hsi) {                                                                                     \
         if (P.mask) launch_cost_views<E, true, true>(desc, lutA, lutA_n, lutB, vol, P, ctr, ctr_base, st);  \
         else launch_cost_views<E, true, false>(desc, lutA, lutA_n, lutB, vol, P, ctr, ctr_base, st);        \

@@ -13,6 +13,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <type_traits>
+
 namespace tsm {
 
 constexpr int kWave = 64;
@@ -77,9 +79,14 @@ struct PairOut {
 };
 
 // Move arena pointers from pair 0's slot to pair `pair`'s (null pointers stay null).
+// Byte-pointer arithmetic, not an integer round trip: the shifted pointer keeps the
+// kernel argument's provenance, so the compiler still knows it addresses global memory
+// and emits global_* instead of flat_* accesses (a flat access also counts against
+// lgkmcnt, so every LDS wait after it would wait for the memory access too).
 template <class Ptr>
 __device__ __forceinline__ void pair_shift1(size_t off, Ptr& p) {
-    if (p) p = (Ptr)(reinterpret_cast<uintptr_t>(p) + off);
+    using B = std::conditional_t<std::is_const_v<std::remove_pointer_t<Ptr>>, const char*, char*>;
+    if (p) p = (Ptr)((B)p + off);
 }
 template <class... Ptr>
 __device__ __forceinline__ void pair_shift(unsigned pair, size_t pstride, Ptr&... p) {
