@@ -691,6 +691,9 @@ __global__ __launch_bounds__(CM_THREADS) __attribute__((amdgpu_waves_per_eu(4)))
         xcol[p] = r3.x;
     }
     __syncthreads();
+#ifdef TSM_EXP_CM_STAGEONLY  // timing only: the staging phase alone
+    return;
+#endif
 
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
     const int j0 = seg_lo + CM_JB * wave;
@@ -876,9 +879,9 @@ __global__ __launch_bounds__(CM_THREADS) __attribute__((amdgpu_waves_per_eu(4)))
         }
     } else
 #endif
-    {
+#ifdef TSM_EXP_CM_TILESTORE
+    {  // experiment: every tile stores its own cells (4 x 64-B runs per store)
     for (int m = 0; m < min(f_lo, M + 1); ++m) tile(m, IC<0>{});
-    // fast tiles two at a time: tile m + 1's MFMAs overlap tile m's epilogue
     auto fast_run = [&](auto Fc) {
         int m = f_lo;
         for (; m < f_hi; m += 2) {
@@ -892,6 +895,79 @@ __global__ __launch_bounds__(CM_THREADS) __attribute__((amdgpu_waves_per_eu(4)))
     else fast_run(IC<2>{});
     for (int m = max(f_hi + 1, min(f_lo, M + 1)); m <= M; ++m) tile(m, IC<0>{});
     }
+#else
+    {
+    // Tiles 1.. in groups of four.  A tile's store would write 4 pixels x 64 B; instead the
+    // group's four results per output row r are transposed between the lane rows and the
+    // registers (v_permlane32_swap + v_permlane16_swap, 4 instructions per r), so lane row
+    // t of register g holds tile m0 + t of pixel j0 + 4 g + r: one store then writes 64
+    // consecutive labels (256 contiguous bytes) of one pixel.  Byte offset of (lane, g, r):
+    // CM_BIAS + 4 (j Lp + k) = ab + st (4 g + r) + 64 m0, VGPR part ab, the rest uniform.
+    const int kt = v == 0 ? CM_JB * grp - col : CM_JB * grp + col;  // k = kt + kg (4g + r) + 16 m0
+    const int kg = v == 0 ? 1 : -1;
+    const uint32_t ab = CM_BIAS + 4u * (uint32_t)(j0 * Lp + kt);
+    const int st = 4 * (Lp + kg);
+    auto group = [&](int m0, int cnt, auto FASTc) {
+        constexpr bool FAST = decltype(FASTc)::value != 0;
+        float X[4][4];  // [tile t][row r]
+#pragma unroll
+        for (int t = 0; t < 4; ++t) {
+            if (t < cnt) {
+                const int m = m0 + t;
+                const v4f_ acc = mma(m);
+                const int p0 = pb + ps * m;
+                const uint32_t vc = cl[p0];
+                bool xok = true;
+                if (!FAST) {
+                    const int x = xs0 + p0 + col;
+                    xok = x - hw >= 0 && x + hw < W;
+                }
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    const uint32_t cen4 = (uint32_t)acc[r];  // 4 x census: byte offset into sB
+                    const uint32_t ad4 = __builtin_amdgcn_sad_u8(fc[r], vc, 0u) << 2;
+                    const float c = *reinterpret_cast<const float*>(reinterpret_cast<const char*>(sA2) + ad4) -
+                                    *reinterpret_cast<const float*>(reinterpret_cast<const char*>(sB) + cen4);
+                    X[t][r] = (FAST || (fo[r] && xok)) ? c : 2.f;
+                }
+            } else {
+#pragma unroll
+                for (int r = 0; r < 4; ++r) X[t][r] = 0.f;  // past tile M: every store masked
+            }
+        }
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            uint32_t R0 = __float_as_uint(X[0][r]), R1 = __float_as_uint(X[1][r]);
+            uint32_t R2 = __float_as_uint(X[2][r]), R3 = __float_as_uint(X[3][r]);
+            auto a = __builtin_amdgcn_permlane32_swap(R0, R2, false, false);  // rows 2,3 <-> 0,1
+            R0 = a[0]; R2 = a[1];
+            a = __builtin_amdgcn_permlane32_swap(R1, R3, false, false);
+            R1 = a[0]; R3 = a[1];
+            a = __builtin_amdgcn_permlane16_swap(R0, R1, false, false);  // odd rows <-> even rows
+            R0 = a[0]; R1 = a[1];
+            a = __builtin_amdgcn_permlane16_swap(R2, R3, false, false);
+            R2 = a[0]; R3 = a[1];
+            const uint32_t Rg[4] = {R0, R1, R2, R3};
+#pragma unroll
+            for (int g = 0; g < 4; ++g) {
+                const int n = 4 * g + r;  // pixel j0 + n
+                int voff = (int)ab;
+                if (!FAST) {
+                    const int k = kt + kg * n + CM_JB * m0;
+                    voff = ((unsigned)k < (unsigned)L && grp < cnt && j0 + n < W) ? voff : -1;
+                }
+                __builtin_amdgcn_raw_buffer_store_b32(Rg[g], vrs, voff, 64 * m0 + st * n, 0);
+            }
+        }
+    };
+    tile(0, IC<0>{});  // the band edge k = -15..15 (one tile, per-cell stores)
+    for (int m0 = 1; m0 <= M; m0 += 4) {
+        const int cnt = min(4, M + 1 - m0);
+        if (cnt == 4 && m0 >= f_lo && m0 + 3 <= f_hi) group(m0, 4, IC<1>{});
+        else group(m0, cnt, IC<0>{});
+    }
+    }
+#endif
     // padding labels L..Lp-1: +inf (lane = pixel)
     if (Lp > L && lane < CM_JB && j0 + lane < W) {
         for (int k = L; k < Lp; ++k)
