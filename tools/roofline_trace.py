@@ -11,7 +11,7 @@ import csv
 import json
 import sys
 
-rows = [r for r in csv.DictReader(open(sys.argv[1])) if "k_cost_walk" in r["Kernel_Name"]]
+rows = [r for r in csv.DictReader(open(sys.argv[1])) if "k_cost_walk" in r["Kernel_Name"] or "k_cost_mfma" in r["Kernel_Name"]]
 batch = int(sys.argv[2]) if len(sys.argv) > 2 else 8
 rows.sort(key=lambda r: int(r["Start_Timestamp"]))
 last = rows[-batch:]
