@@ -1265,7 +1265,10 @@ __device__ __forceinline__ f32x4 fmam(f32x4 acc, f32x4 x, float m) {
 // 1 if k < len else 0 (len, k small non-negative integers as floats)
 __device__ __forceinline__ float wmask(float lenf, float k) { return __builtin_amdgcn_fmed3f(lenf - k, 0.f, 1.f); }
 
-template <bool FUSED, bool DIV, int QT>
+// WA / WB (roles A / B): 0 = the masked VGPR window above, 1 = v6's scalar window loop
+// (uniform offsets and lengths in SGPRs).  Mixing the two moves a role's bookkeeping to
+// the issue port the other role leaves idle (the CU issues one SALU and one VALU a cycle).
+template <bool FUSED, bool DIV, int QT, int WA = 0, int WB = 0>
 __global__ __launch_bounds__(AX_THREADS) void k_agg_v7(AggStream S, DevParams Pk) {
     const DevParams P = Pk;
     pair_shift(blockIdx.z, P.pstride, S.vol, S.arms, S.ws, S.pk, S.rcp);
@@ -1360,6 +1363,35 @@ __global__ __launch_bounds__(AX_THREADS) void k_agg_v7(AggStream S, DevParams Pk
         const uint32_t t = slotQs - lo * Qs;
         return min(t, t + span);
     };
+    // v6's window: blocks of 4 at immediate offsets (the mirror slots keep a block
+    // contiguous), the 1-3 remaining pixels under uniform branches; `off` ring-relative
+    auto window_s = [&](const char* base, uint32_t off, int len, uint32_t span) -> f32x4 {
+        f32x4 acc = f32x4{0.f, 0.f, 0.f, 0.f};
+        for (int nb = len >> 2; nb > 0; --nb) {
+            const char* p = base + off;
+            const f32x4 x0 = *reinterpret_cast<const f32x4*>(p);
+            const f32x4 x1 = *reinterpret_cast<const f32x4*>(p + Qs);
+            const f32x4 x2 = *reinterpret_cast<const f32x4*>(p + 2 * Qs);
+            const f32x4 x3 = *reinterpret_cast<const f32x4*>(p + 3 * Qs);
+            acc += x0;
+            acc += x1;
+            acc += x2;
+            acc += x3;
+            off += 4 * Qs;
+            off = off >= span ? off - span : off;
+        }
+        const int r = len & 3;
+        if (r) {
+            const char* p = base + off;
+            const f32x4 x0 = *reinterpret_cast<const f32x4*>(p);
+            const f32x4 x1 = *reinterpret_cast<const f32x4*>(p + Qs);
+            const f32x4 x2 = *reinterpret_cast<const f32x4*>(p + 2 * Qs);
+            acc += x0;
+            if (r > 1) acc += x1;
+            if (r > 2) acc += x2;
+        }
+        return acc;
+    };
     const char* mbase = lds + meta_off + (uint32_t)w * AX_MW * 4;  // this wave's pixel column of the meta ring
 
     if (roleA) {
@@ -1432,16 +1464,29 @@ __global__ __launch_bounds__(AX_THREADS) void k_agg_v7(AggStream S, DevParams Pk
                 land(rv[u], rma[u], rmy[u], s + AS_AHEAD);
                 issue(u);
                 // pass A on chunk s, pixel w (ring1 slot u*8 + w): descriptor in VGPRs
-                const uint32_t pk = vopaque(mA.x);
-                const float a_y = __uint_as_float(vopaque(mA.y));
-                const uint32_t lo = pk & 0xffu, hi = (pk >> 8) & 0xffu;
-                const float a_b = (float)(pk >> 16);
-                const uint32_t len_v = lo + hi + 1;
-                const int len = (int)__builtin_amdgcn_readfirstlane(len_v);
-                const uint32_t rel = wstart((uint32_t)(u * AS_SEG) * Qs + wv * Qs, lo, span1);
-                mA = *reinterpret_cast<const u32x2*>(mbase + ((u + 1) % AX_MC) * mstep);  // chunk s + 1 (landed)
-                f32x4 acc = window(r1b, rel, len_v, len, span1);
-                if (DIV) acc = div_ws(acc, a_b, a_y);
+                f32x4 acc;
+                if constexpr (WA == 0) {
+                    const uint32_t pk = vopaque(mA.x);
+                    const float a_y = __uint_as_float(vopaque(mA.y));
+                    const uint32_t lo = pk & 0xffu, hi = (pk >> 8) & 0xffu;
+                    const float a_b = (float)(pk >> 16);
+                    const uint32_t len_v = lo + hi + 1;
+                    const int len = (int)__builtin_amdgcn_readfirstlane(len_v);
+                    const uint32_t rel = wstart((uint32_t)(u * AS_SEG) * Qs + wv * Qs, lo, span1);
+                    mA = *reinterpret_cast<const u32x2*>(mbase + ((u + 1) % AX_MC) * mstep);  // chunk s + 1 (landed)
+                    acc = window(r1b, rel, len_v, len, span1);
+                    if (DIV) acc = div_ws(acc, a_b, a_y);
+                } else {
+                    const uint32_t arm = __builtin_amdgcn_readfirstlane(mA.x);
+                    const float a_y = __uint_as_float(__builtin_amdgcn_readfirstlane(mA.y));
+                    const float a_b = (float)(int)(arm >> 16);
+                    const int lo = (int)(arm & 0xffu), hi = (int)((arm >> 8) & 0xffu);
+                    int st = u * AS_SEG + w - lo;
+                    st = st < 0 ? st + AS_RP1 : st;
+                    mA = *reinterpret_cast<const u32x2*>(mbase + ((u + 1) % AX_MC) * mstep);  // chunk s + 1 (landed)
+                    acc = window_s(r1b, (uint32_t)st * Qs, lo + hi + 1, span1);
+                    if (DIV) acc = div_ws(acc, a_b, a_y);
+                }
                 // every step writes its ring2 slot (chunks past the stream are never read)
                 *reinterpret_cast<f32x4*>(r2w + (uint32_t)(u * AS_SEG) * Qs) = acc;
                 if (u == 0 && w < AX_MIR) *reinterpret_cast<f32x4*>(r2w + (uint32_t)AS_RP2 * Qs) = acc;
@@ -1471,7 +1516,7 @@ __global__ __launch_bounds__(AX_THREADS) void k_agg_v7(AggStream S, DevParams Pk
         for (int u = 0; u < AX_D; ++u) {
             const int s = b * AX_D + u;
             const int ub = (u - lag + 2 * AX_D) % AX_D;  // ring / meta chunk slot of chunk s - lag
-            const uint32_t pk = vopaque(mB);
+            const uint32_t pk = WB == 0 ? vopaque(mB) : __builtin_amdgcn_readfirstlane(mB);
             const uint32_t lo = pk & 0xffu, hi = (pk >> 8) & 0xffu;
             const uint32_t len_v = lo + hi + 1;
             const uint32_t slotQs = (uint32_t)(ub * AS_SEG) * Qs + wv * Qs;
@@ -1480,7 +1525,11 @@ __global__ __launch_bounds__(AX_THREADS) void k_agg_v7(AggStream S, DevParams Pk
             if (sb >= 0 && sb < nch) {
                 if (o_cc * AS_SEG + w < S.n) {
                     f32x4 acc;
-                    if (FUSED) {
+                    if (FUSED && WB == 1) {
+                        int st = ub * AS_SEG + w - (int)lo;
+                        st = st < 0 ? st + AS_RP2 : st;
+                        acc = window_s(r2b, (uint32_t)st * Qs, (int)len_v, span2);
+                    } else if (FUSED) {
                         const int len = (int)__builtin_amdgcn_readfirstlane(len_v);
                         acc = window(r2b, wstart(slotQs, lo, span2), len_v, len, span2);
                     } else {
@@ -1579,7 +1628,21 @@ int launch_agg_stream(float* vol, const uint32_t* arms, const int32_t* ws, const
                 (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
                 hipLaunchKernelGGL(kern, sgrid, dim3(AX_THREADS), slds, st, S, P);
             };
-            if (Q == 49 && nslice == 1) {
+            // TSM_AGG_MIX=<A><B>, each v (masked VGPR window) or s (scalar window loop)
+            static const int mix = [] {
+                const char* e = getenv("TSM_AGG_MIX");
+                return !e || !e[0] || !e[1] ? 0 : (e[0] == 's' ? 2 : 0) + (e[1] == 's' ? 1 : 0);
+            }();
+            if (Q == 49 && nslice == 1 && mix == 2) {  // A scalar, B vector
+                if (fused) div ? go(k_agg_v7<true, true, 49, 1, 0>) : go(k_agg_v7<true, false, 49, 1, 0>);
+                else div ? go(k_agg_v7<false, true, 49, 1, 0>) : go(k_agg_v7<false, false, 49, 1, 0>);
+            } else if (Q == 49 && nslice == 1 && mix == 1) {  // A vector, B scalar
+                if (fused) div ? go(k_agg_v7<true, true, 49, 0, 1>) : go(k_agg_v7<true, false, 49, 0, 1>);
+                else div ? go(k_agg_v7<false, true, 49, 0, 1>) : go(k_agg_v7<false, false, 49, 0, 1>);
+            } else if (Q == 49 && nslice == 1 && mix == 3) {  // both scalar (v6 windows, v7 staging)
+                if (fused) div ? go(k_agg_v7<true, true, 49, 1, 1>) : go(k_agg_v7<true, false, 49, 1, 1>);
+                else div ? go(k_agg_v7<false, true, 49, 1, 1>) : go(k_agg_v7<false, false, 49, 1, 1>);
+            } else if (Q == 49 && nslice == 1) {
                 if (fused) div ? go(k_agg_v7<true, true, 49>) : go(k_agg_v7<true, false, 49>);
                 else div ? go(k_agg_v7<false, true, 49>) : go(k_agg_v7<false, false, 49>);
             } else {

@@ -625,7 +625,10 @@ constexpr int CM_WAVES = 8;
 constexpr int CM_THREADS = CM_WAVES * 64;
 constexpr int CM_JB = 16;                   // pixels per wave (one tile row block)
 constexpr int CM_SEG = CM_WAVES * CM_JB;    // pixels per unit
-constexpr uint32_t CM_BIAS = 64;            // store buffer starts this many bytes before the row
+constexpr uint32_t CM_BIAS = 64;
+#ifndef TSM_CM_STAUX
+#define TSM_CM_STAUX 0  // cache-policy bits of the volume stores (experiments: 2 = nt)
+#endif            // store buffer starts this many bytes before the row
 
 typedef int v8i_ __attribute__((ext_vector_type(8)));
 typedef float v4f_ __attribute__((ext_vector_type(4)));
@@ -821,7 +824,7 @@ __global__ __launch_bounds__(CM_THREADS) __attribute__((amdgpu_waves_per_eu(4)))
 #ifdef TSM_EXP_CM_NOSTORE
                 if (cr == -12345.f)
 #endif
-                __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(cr), vrs, off, mo, 0);
+                __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(cr), vrs, off, mo, TSM_CM_STAUX);
             }
         }
     };
@@ -956,7 +959,7 @@ __global__ __launch_bounds__(CM_THREADS) __attribute__((amdgpu_waves_per_eu(4)))
                     const int k = kt + kg * n + CM_JB * m0;
                     voff = ((unsigned)k < (unsigned)L && grp < cnt && j0 + n < W) ? voff : -1;
                 }
-                __builtin_amdgcn_raw_buffer_store_b32(Rg[g], vrs, voff, 64 * m0 + st * n, 0);
+                __builtin_amdgcn_raw_buffer_store_b32(Rg[g], vrs, voff, 64 * m0 + st * n, TSM_CM_STAUX);
             }
         }
     };
