@@ -336,7 +336,8 @@ __global__ __launch_bounds__(CW_THREADS) __attribute__((amdgpu_waves_per_eu(E ==
     };
     for (int c = 0; c < slots; c += CW_CHUNK) dma_chunk(c);
 
-    for (int i = threadIdx.x; i < lutA_n; i += CW_THREADS) sA[i] = lutA[i];
+    // sA holds 2 - A[ad]: the reference's (2 - A) - B with its first subtraction done once
+    for (int i = threadIdx.x; i < lutA_n; i += CW_THREADS) sA[i] = 2.f - lutA[i];
     for (int i = threadIdx.x; i < 2 * CW_LUTB; i += CW_THREADS)
         sB[i] = i < 188 ? lutB[i] : (i >= CW_LUTB ? -__int_as_float(0x7f800000) : 0.f);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // ring prologue landed (LDS-DMA)
@@ -443,7 +444,7 @@ __global__ __launch_bounds__(CW_THREADS) __attribute__((amdgpu_waves_per_eu(E ==
 #ifdef TSM_EXP_NOLUT
             c[e] = (float)ai - (float)cen[e];
 #else
-            c[e] = 2.f - sA[ai] - sB[cen[e]];
+            c[e] = sA[ai] - sB[cen[e]];
 #endif
         }
         // border cells (either 9x7 window leaves the image, :562-566) and masked own
@@ -583,7 +584,7 @@ __global__ __launch_bounds__(CW_THREADS) __attribute__((amdgpu_waves_per_eu(E ==
                         const int hd = (int)__builtin_amdgcn_sad_u8(fc & 0xffu, vc & 0xffu, 0u);
                         ai = 2 * min(hd, 255 - hd) + 5 * (int)__builtin_amdgcn_sad_u8(fc & 0xffff00u, vc & 0xffff00u, 0u);
                     }
-                    const float c = 2.f - sA[ai] - sB[cen];
+                    const float c = sA[ai] - sB[cen];
                     c4[t] = (fixed_ok && k >= klo && k <= khi) ? c : 2.f;
                 }
             }
@@ -1107,10 +1108,12 @@ int launch_cost_volume(const uint32_t* img, const uint32_t* desc, const float* l
                        uint32_t& ctr_base, hipStream_t st) {
     (void)img;
     const bool hsi = P.color_model == 1;
-    // RGB without mask mode: the matrix-core build (TSM_COST_MFMA=0 keeps the walk)
+    // The product path is the walk (north_star: census by popcount, no MFMA).  The
+    // matrix-core build is a measured experiment kept for the record: TSM_COST_MFMA=1
+    // (RGB without mask mode) selects it.
     static const bool use_mfma = [] {
         const char* e = getenv("TSM_COST_MFMA");
-        return !(e && e[0] == '0');
+        return e && e[0] == '1';
     }();
     const size_t mlds = cost_mfma_lds_bytes(P);
     if (use_mfma && !hsi && !P.mask && lutA_n <= 768 && mlds + 4 * (768 + 192) <= 160 * 1024) {

@@ -1,9 +1,9 @@
 #!/usr/bin/env python3
 """HBM bytes per cost-volume launch from two rocprofv3 --pmc passes (FETCH_SIZE, WRITE_SIZE;
-separate passes, kernel filter k_cost_mfma), with the gfx950 correction of the
+separate passes, kernel filter $KREGEX), with the gfx950 correction of the
 microarchitecture guide: FETCH_SIZE counts 64 B per 128-B request of a wide coalesced
 read, so it is doubled; WRITE_SIZE is exact for 16-B-per-lane streaming stores.  Both
-are in KiB.  Usage: pmc_cost_json.py FETCH.csv WRITE.csv OUT.json"""
+are in KiB.  Usage: pmc_cost_json.py FETCH.csv WRITE.csv OUT.json [kernel]"""
 import collections
 import csv
 import json
@@ -23,7 +23,7 @@ write = per_dispatch(sys.argv[2], "WRITE_SIZE")
 f_kib = sum(fetch) / len(fetch)
 w_kib = sum(write) / len(write)
 out = {
-    "kernel": "k_cost_mfma<12> (config B: 1242x375, L=193, both views, one launch)",
+    "kernel": (sys.argv[4] if len(sys.argv) > 4 else "k_cost_walk<3,false,false,0>") + " (config B: 1242x375, L=193, both views, one launch)",
     "dispatches": {"fetch_pass": len(fetch), "write_pass": len(write)},
     "fetch_size_kib_raw": f_kib,
     "write_size_kib": w_kib,
