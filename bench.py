@@ -43,8 +43,8 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=2)
-    ap.add_argument("--batch", type=int, default=64, help="pairs per GPU per step")
-    ap.add_argument("--concurrency", type=int, default=32,
+    ap.add_argument("--batch", type=int, default=128, help="pairs per GPU per step")
+    ap.add_argument("--concurrency", type=int, default=64,
                     help="pairs per group (one pipeline per group; consecutive groups run on two streams)")
     ap.add_argument("--height", type=int, default=375)
     ap.add_argument("--width", type=int, default=1242)

@@ -320,3 +320,42 @@ def test_full_size_configs_bit_exact(matcher, tsm, cfg):
     assert list(d_g.shape) == gold["shape"]
     assert abs(float((d_g >= 0).mean()) - gold["valid_fraction"]) < 1e-12
     assert hashlib.sha256(d_g.tobytes()).hexdigest() == gold["sha256"]
+
+
+MFMA_CHILD = r"""
+import sys
+import numpy as np
+sys.path.insert(0, sys.argv[1])
+import tea_stereo_matching_amd as T
+out = sys.argv[2]
+res = {}
+m = T.ADCensus(0)
+for i, (seed, H, W, mn, mx) in enumerate(((31, 24, 300, 0, 192), (2, 120, 160, 0, 48), (3, 97, 131, 0, 64))):
+    left, right = T.synthetic.make_scene(seed, H, W, mx - mn + 1)[:2]
+    m.setMatchingStrategy(T.ColorModel(0), False, False)
+    m.setMinMaxDisparity(mn, mx)
+    _, g = m.compute_debug(left, right, ("cost_init",))
+    res[f"c{i}"] = g["cost_init"]
+m.close()
+np.savez(out, **res)
+"""
+
+
+def test_cost_mfma_experiment_bit_exact(oracle, tmp_path):
+    """The opt-in matrix-core cost build (TSM_COST_MFMA=1, an experiment kept beside the
+    popcount walk) produces the oracle's initial volume bit for bit.  The switch is read
+    once per process, so the build runs in a child process."""
+    import subprocess
+    import sys
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    out = str(tmp_path / "mfma.npz")
+    env = dict(os.environ, TSM_COST_MFMA="1")
+    r = subprocess.run([sys.executable, "-c", MFMA_CHILD, root, out], env=env, capture_output=True,
+                       text=True, timeout=120)
+    assert r.returncode == 0, r.stderr[-2000:]
+    got = np.load(out)
+    for i, (seed, H, W, mn, mx) in enumerate(((31, 24, 300, 0, 192), (2, 120, 160, 0, 48), (3, 97, 131, 0, 64))):
+        left, right = _synthetic(__import__("tea_stereo_matching_amd"), seed, H, W, mx - mn + 1)
+        _, o = oracle.compute(left, right, _oracle_params(oracle, oracle.RGB, mn, mx), ("cost_init",))
+        assert np.array_equal(got[f"c{i}"], o["cost_init"]), f"case {i}"

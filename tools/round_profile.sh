@@ -12,5 +12,5 @@ rc=$?; echo "bench rc=$rc"; [ $rc -ne 0 ] && { tail -20 gpurun_out/${TAG}_bench.
 grep '^{' gpurun_out/${TAG}_bench.log | tail -1 > gpurun_out/${TAG}_bench.json
 timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/${TAG}_prof -o run -- python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline > gpurun_out/${TAG}_prof.log 2>&1
 rc=$?; echo "prof rc=$rc"; [ $rc -ne 0 ] && { tail -20 gpurun_out/${TAG}_prof.log; exit $rc; }
-python3 tools/roofline_trace.py gpurun_out/${TAG}_prof/run_kernel_trace.csv 64 > gpurun_out/${TAG}_cost_roofline_trace.json
+python3 tools/roofline_trace.py gpurun_out/${TAG}_prof/run_kernel_trace.csv 128 > gpurun_out/${TAG}_cost_roofline_trace.json
 cat gpurun_out/${TAG}_bench.json
