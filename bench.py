@@ -211,6 +211,20 @@ def main():
             "timing": f"HIP events around each cost-volume launch, {cost_n} launches, one pipeline (no co-running kernels)",
         },
     }
+    # whole pipeline against the HBM roof (SURVEY §8d secondary): B_pipe = 18 volume
+    # transfers of 2*L*N*4 B a pair (1 build write + aggregation 4 x (R+W) + scanline
+    # 4 x (R+W) + 1 WTA read); achieved = B_pipe x this GPU's pairs/s
+    b_pipe = 18 * 2 * L * N * 4
+    line["pipeline_roofline"] = {
+        "bound": "hbm",
+        "algorithmic_bytes_per_pair": b_pipe,
+        "achieved": round(b_pipe * value / world / 1e9, 1),
+        "peak": HBM_PEAK_GBS,
+        "unit": "GB/s",
+        "frac": round(b_pipe * value / world / 1e9 / HBM_PEAK_GBS, 4),
+    }
+    if rank == 0:
+        line["hbm_calibration"] = hbm_calibration(L * N * 2 * 4)
     if rank == 0 and not args.no_ops:
         line["next_rows"] = ops_leg(tsm, outs, lefts, H, W)
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
@@ -224,6 +238,36 @@ def main():
         print(json.dumps(line), flush=True)
     if world > 1:
         dist.destroy_process_group()
+
+
+def hbm_calibration(nbytes, reps=20):
+    """Measured HBM rates on this GPU (untimed for `value`): a write-only fill and a copy
+    (read + write) over a buffer the size of one pair's two-view volume, torch kernels
+    timed with events -- the achievable rates the roofline fractions sit under."""
+    import torch
+
+    n = nbytes // 4
+    x = torch.empty(n, dtype=torch.float32, device="cuda")
+    y = torch.empty_like(x)
+    x.fill_(1.0)
+
+    def rate(fn, moved):
+        for _ in range(3):
+            fn()
+        s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        s.record()
+        for _ in range(reps):
+            fn()
+        e.record()
+        torch.cuda.synchronize()
+        return round(moved / (s.elapsed_time(e) / reps / 1e3) / 1e9, 1)
+
+    out = {"buffer_bytes": n * 4, "write_GBps": rate(lambda: x.fill_(2.0), n * 4),
+           "copy_GBps": rate(lambda: y.copy_(x), 2 * n * 4), "unit": "GB/s",
+           "timing": f"torch fill_ / copy_, {reps} back-to-back launches, HIP events"}
+    del x, y
+    torch.cuda.empty_cache()
+    return out
 
 
 def ops_leg(tsm, outs, lefts, H, W, iters=50):
