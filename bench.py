@@ -147,6 +147,22 @@ def main():
     stages_conc = m.stageTimes()
     elapsed = Dd.max_over_ranks(elapsed, world, dev)
 
+    # Host-buffer leg (untimed for `value`): the same batch handed over as host (pageable
+    # numpy) images and returned to host arrays, i.e. the C ABI's tsm_adc_compute_batch with
+    # its H2D / D2H copies -- the PCIe-inclusive rate of the drop-in boundary.
+    host_leg = None
+    if rank == 0:
+        lh = [t.cpu().numpy() for t in lefts]
+        rh = [t.cpu().numpy() for t in rights]
+        m.compute_batch(lh, rh)
+        t1 = time.perf_counter()
+        for _ in range(2):
+            m.compute_batch(lh, rh)
+        dt = (time.perf_counter() - t1) / 2
+        host_leg = {"value": round(B / dt, 3), "unit": "pairs/s",
+                    "timing": f"tsm_adc_compute_batch on {B} pageable host pairs (H2D + pipeline + D2H), "
+                              "mean of 2 batches after 1 warm-up, this GPU"}
+
     # Roofline phase (untimed): the same pairs through ONE pipeline, so the cost-volume
     # launches run alone on the GPU and their HIP-event durations are the kernel's own
     # (in the timed region a second pipeline's kernels share the GPU with them).
@@ -224,6 +240,7 @@ def main():
         "frac": round(b_pipe * value / world / 1e9 / HBM_PEAK_GBS, 4),
     }
     if rank == 0:
+        line["host_buffers"] = host_leg
         line["hbm_calibration"] = hbm_calibration(L * N * 2 * 4)
     if rank == 0 and not args.no_ops:
         line["next_rows"] = ops_leg(tsm, outs, lefts, H, W)

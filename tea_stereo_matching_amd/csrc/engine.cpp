@@ -97,6 +97,15 @@ struct Workspace {
     size_t in_cap = 0;
     int in_slots = 0;
     float* out_dev = nullptr;
+    // host-batch staging in pinned memory (tsm_adc_compute_batch): the caller's pageable
+    // images are copied in by the host and its outputs copied out once the group's stream
+    // has drained, so every device copy is asynchronous and groups overlap
+    uint8_t* h_in = nullptr;       // [2][slots][rows * cols * 3]: left images, then right
+    float* h_out = nullptr;        // [slots][rows * cols]
+    size_t h_in_bytes = 0, h_out_bytes = 0;
+    std::vector<float*> pend_out;  // the caller's outputs of the group in flight
+    int pend_rows = 0, pend_cols = 0;
+    size_t pend_step = 0;
     // pair 0's buffers in the arena (pair p: + p * slot)
     uint32_t* img_orig = nullptr;  // [2][H][W] packed BGR
     uint32_t* img = nullptr;       // [2][H][W] matched images (== img_orig for RGB)
@@ -661,10 +670,30 @@ int stream_after(tsm_adc* h, Workspace* w, hipStream_t before, hipStream_t after
 
 // After an error in a batch, queued copies may still read/write caller buffers: drain
 // every workspace stream before handing the error back (keeps the first error message).
+// Pinned output staging of the group that ran on w -> the caller's buffers (row by row
+// when the caller's row step is wider).  The stream must have drained.
+void copy_out_pending(Workspace* w) {
+    const size_t rowb = (size_t)w->pend_cols * 4, img = (size_t)w->pend_rows * w->pend_cols;
+    for (size_t j = 0; j < w->pend_out.size(); ++j) {
+        const float* src = w->h_out + j * img;
+        char* dst = reinterpret_cast<char*>(w->pend_out[j]);
+        if (w->pend_step == rowb) {
+            std::memcpy(dst, src, rowb * w->pend_rows);
+        } else {
+            for (int y = 0; y < w->pend_rows; ++y) std::memcpy(dst + y * w->pend_step, src + (size_t)y * w->pend_cols, rowb);
+        }
+    }
+    w->pend_out.clear();
+}
+
 int drain_after_error(tsm_adc* h, int rc) {
     const std::string msg = h->err;
-    for (Workspace* w : h->ws)
-        if (w->stream) hipStreamSynchronize(w->stream);
+    for (Workspace* w : h->ws) {
+        // groups already enqueued by a failing host batch still hand their outputs over
+        // (they were validated and ran); nothing is left pending for a later call
+        if (w->stream && hipStreamSynchronize(w->stream) == hipSuccess) copy_out_pending(w);
+        w->pend_out.clear();
+    }
     h->err = msg;
     return rc;
 }
@@ -698,6 +727,8 @@ int tsm_adc_destroy(tsm_adc* h) {
         if (w->in_left) hipFree(w->in_left);
         if (w->in_right) hipFree(w->in_right);
         if (w->out_dev) hipFree(w->out_dev);
+        if (w->h_in) hipHostFree(w->h_in);
+        if (w->h_out) hipHostFree(w->h_out);
         for (auto& pe : w->pending) for (hipEvent_t e : pe.first) hipEventDestroy(e);
         for (hipEvent_t e : w->ev_pool) hipEventDestroy(e);
         if (w->stream) hipStreamDestroy(w->stream);
@@ -903,6 +934,34 @@ static int group_plan(tsm_adc* h, int n, int& K, int& nws) {
 }
 
 // Group g's stream waits for group g-1's stagger point (other workspace's stream).
+// Pinned host staging of a group of K pairs (grown, never shrunk).
+static int ensure_pinned(tsm_adc* h, Workspace* w, int rows, int cols, int K) {
+    const size_t in_need = (size_t)2 * K * rows * cols * 3, out_need = (size_t)K * rows * cols * 4;
+    if (w->h_in_bytes < in_need) {
+        if (w->h_in) hipHostFree(w->h_in);
+        w->h_in = nullptr;
+        w->h_in_bytes = 0;
+        HIP_OK(hipHostMalloc((void**)&w->h_in, in_need, hipHostMallocDefault));
+        w->h_in_bytes = in_need;
+    }
+    if (w->h_out_bytes < out_need) {
+        if (w->h_out) hipHostFree(w->h_out);
+        w->h_out = nullptr;
+        w->h_out_bytes = 0;
+        HIP_OK(hipHostMalloc((void**)&w->h_out, out_need, hipHostMallocDefault));
+        w->h_out_bytes = out_need;
+    }
+    return TSM_OK;
+}
+
+// Wait for the group in flight on w and hand its outputs over.
+static int flush_outputs(tsm_adc* h, Workspace* w) {
+    if (w->pend_out.empty()) return TSM_OK;
+    HIP_OK(hipStreamSynchronize(w->stream));
+    copy_out_pending(w);
+    return TSM_OK;
+}
+
 static int wait_previous_group(tsm_adc* h, int g, int nws) {
     if (g == 0 || nws < 2 || group_stagger() <= 0) return TSM_OK;
     Workspace* prev = h->ws[(g - 1) % nws];
@@ -957,27 +1016,42 @@ int tsm_adc_compute_batch(tsm_adc* h, int n, const uint8_t* const* ls, const uin
             if (!outs[i] || out_step < (size_t)cols * 4)
                 return drain_after_error(h, fail(h, TSM_ERR_ARGUMENT, "output buffer"));
         }
+        // the group before on this workspace hands its outputs over first (its pinned
+        // staging is reused below); the other workspace's group keeps running meanwhile
+        if ((rc = flush_outputs(h, w)) != TSM_OK) return drain_after_error(h, rc);
         if ((rc = ensure_workspace(h, w, rows, cols, K)) != TSM_OK) return drain_after_error(h, rc);
         if ((rc = ensure_input_staging(h, w, rows, (size_t)cols * 3, cols, K)) != TSM_OK)
             return drain_after_error(h, rc);
+        if ((rc = ensure_pinned(h, w, rows, cols, K)) != TSM_OK) return drain_after_error(h, rc);
         if ((rc = wait_previous_group(h, g, nws)) != TSM_OK) return drain_after_error(h, rc);
         PairIn in{};
         PairOut po{};
+        const size_t rowb = (size_t)cols * 3, img = rowb * rows;
         for (int j = 0; j < k; ++j) {
-            if ((rc = stage_host_pair(h, w, j, ls[i0 + j], rs[i0 + j], rows, cols, step, in)) != TSM_OK)
-                return drain_after_error(h, rc);
+            for (int side = 0; side < 2; ++side) {  // pageable -> pinned (host), pinned -> HBM (async)
+                const uint8_t* src = side ? rs[i0 + j] : ls[i0 + j];
+                uint8_t* pin = w->h_in + ((size_t)side * K + j) * img;
+                if (step == rowb) std::memcpy(pin, src, img);
+                else for (int y = 0; y < rows; ++y) std::memcpy(pin + y * rowb, src + y * step, rowb);
+                uint8_t* dst = (side ? w->in_right : w->in_left) + (size_t)j * w->in_cap;
+                if (hipMemcpyAsync(dst, pin, img, hipMemcpyHostToDevice, w->stream) != hipSuccess)
+                    return drain_after_error(h, fail(h, TSM_ERR_DEVICE, "hipMemcpyAsync (input)"));
+                (side ? in.right[j] : in.left[j]) = dst;
+            }
             po.out[j] = w->out_dev + (size_t)j * rows * cols;
         }
-        if ((rc = run_pipeline(h, w, k, in, (size_t)cols * 3, po, (size_t)cols * 4, nullptr, w->stream)) != TSM_OK)
+        if ((rc = run_pipeline(h, w, k, in, rowb, po, (size_t)cols * 4, nullptr, w->stream)) != TSM_OK)
             return drain_after_error(h, rc);
-        for (int j = 0; j < k; ++j) {
-            rc = hipMemcpy2DAsync(outs[i0 + j], out_step, po.out[j], (size_t)cols * 4, (size_t)cols * 4, rows,
-                                  hipMemcpyDeviceToHost, w->stream) == hipSuccess ? TSM_OK : TSM_ERR_DEVICE;
-            if (rc != TSM_OK) return drain_after_error(h, fail(h, rc, "hipMemcpy2DAsync (output)"));
-        }
-        // a workspace's staging is reused by the group after next: that group's copies
-        // are queued behind this one's on the same stream
+        rc = hipMemcpyAsync(w->h_out, w->out_dev, (size_t)k * rows * cols * 4, hipMemcpyDeviceToHost, w->stream) ==
+                     hipSuccess ? TSM_OK : TSM_ERR_DEVICE;
+        if (rc != TSM_OK) return drain_after_error(h, fail(h, rc, "hipMemcpyAsync (output)"));
+        w->pend_out.assign(outs + i0, outs + i0 + k);
+        w->pend_rows = rows;
+        w->pend_cols = cols;
+        w->pend_step = out_step;
     }
+    for (Workspace* w : h->ws)
+        if ((rc = flush_outputs(h, w)) != TSM_OK) return drain_after_error(h, rc);
     return tsm_adc_synchronize(h);
 }
 
