@@ -162,6 +162,15 @@ def main():
         host_leg = {"value": round(B / dt, 3), "unit": "pairs/s",
                     "timing": f"tsm_adc_compute_batch on {B} pageable host pairs (H2D + pipeline + D2H), "
                               "mean of 2 batches after 1 warm-up, this GPU"}
+        # one frame at a time through the reference-shaped call (ADCensus::compute on host
+        # images, synchronous): the per-frame latency a single-stream caller sees
+        m.setConcurrency(1)
+        m.compute(lh[0], rh[0])
+        t1 = time.perf_counter()
+        for i in range(10):
+            m.compute(lh[i % B], rh[i % B])
+        host_leg["single_frame_ms"] = round((time.perf_counter() - t1) / 10 * 1e3, 3)
+        m.setConcurrency(args.concurrency)
 
     # Roofline phase (untimed): the same pairs through ONE pipeline, so the cost-volume
     # launches run alone on the GPU and their HIP-event durations are the kernel's own

@@ -874,17 +874,9 @@ int tsm_adc_compute_device(tsm_adc* h, const uint8_t* dl, const uint8_t* dr, int
 }
 
 // H2D of pair i of a host batch into staging slot k of w (device step 3 * cols).
-static int stage_host_pair(tsm_adc* h, Workspace* w, int k, const uint8_t* l, const uint8_t* r, int rows,
-                           int cols, size_t step, PairIn& in) {
-    const size_t dstep = (size_t)cols * 3;
-    uint8_t* dl = w->in_left + (size_t)k * w->in_cap;
-    uint8_t* dr = w->in_right + (size_t)k * w->in_cap;
-    HIP_OK(hipMemcpy2DAsync(dl, dstep, l, step, dstep, rows, hipMemcpyHostToDevice, w->stream));
-    HIP_OK(hipMemcpy2DAsync(dr, dstep, r, step, dstep, rows, hipMemcpyHostToDevice, w->stream));
-    in.left[k] = dl;
-    in.right[k] = dr;
-    return TSM_OK;
-}
+static int ensure_pinned(tsm_adc* h, Workspace* w, int rows, int cols, int K);
+static int stage_pinned_pair(tsm_adc* h, Workspace* w, int K, int j, const uint8_t* l, const uint8_t* r,
+                             int rows, int cols, size_t step, PairIn& in);
 
 static int compute_host(tsm_adc* h, const uint8_t* l, const uint8_t* r, int rows, int cols,
                         size_t step, float* out, size_t out_step, const tsm_adc_dump* dump) {
@@ -896,15 +888,25 @@ static int compute_host(tsm_adc* h, const uint8_t* l, const uint8_t* r, int rows
     Workspace* w = h->ws[0];
     if ((rc = ensure_workspace(h, w, rows, cols, 1)) != TSM_OK) return rc;
     if ((rc = ensure_input_staging(h, w, rows, (size_t)cols * 3, cols, 1)) != TSM_OK) return rc;
+    if ((rc = ensure_pinned(h, w, rows, cols, 1)) != TSM_OK) return rc;
     PairIn in{};
     PairOut po{};
-    if ((rc = stage_host_pair(h, w, 0, l, r, rows, cols, step, in)) != TSM_OK) return rc;
+    // pageable caller buffers go through pinned staging (a pageable copy costs ~6 ms a
+    // config-B frame, the whole pipeline ~4)
+    if ((rc = stage_pinned_pair(h, w, 1, 0, l, r, rows, cols, step, in)) != TSM_OK) return drain_after_error(h, rc);
     po.out[0] = w->out_dev;
     if ((rc = run_pipeline(h, w, 1, in, (size_t)cols * 3, po, (size_t)cols * 4, dump, w->stream)) != TSM_OK)
         return drain_after_error(h, rc);
-    HIP_OK(hipMemcpy2DAsync(out, out_step, w->out_dev, (size_t)cols * 4, (size_t)cols * 4, rows,
-                            hipMemcpyDeviceToHost, w->stream));
-    HIP_OK(hipStreamSynchronize(w->stream));
+    HIP_OK(hipMemcpyAsync(w->h_out, w->out_dev, (size_t)rows * cols * 4, hipMemcpyDeviceToHost, w->stream));
+    w->pend_out.assign(1, out);
+    w->pend_rows = rows;
+    w->pend_cols = cols;
+    w->pend_step = out_step;
+    if (hipStreamSynchronize(w->stream) != hipSuccess) {
+        w->pend_out.clear();
+        return fail(h, TSM_ERR_DEVICE, "hipStreamSynchronize");
+    }
+    copy_out_pending(w);
     collect_profile(h, w);
     return TSM_OK;
 }
@@ -950,6 +952,23 @@ static int ensure_pinned(tsm_adc* h, Workspace* w, int rows, int cols, int K) {
         w->h_out_bytes = 0;
         HIP_OK(hipHostMalloc((void**)&w->h_out, out_need, hipHostMallocDefault));
         w->h_out_bytes = out_need;
+    }
+    return TSM_OK;
+}
+
+// Pair j of a group of K: the caller's (pageable) images -> pinned staging on the host,
+// then an async copy into the workspace's device input slot.
+static int stage_pinned_pair(tsm_adc* h, Workspace* w, int K, int j, const uint8_t* l, const uint8_t* r,
+                             int rows, int cols, size_t step, PairIn& in) {
+    const size_t rowb = (size_t)cols * 3, img = rowb * rows;
+    for (int side = 0; side < 2; ++side) {
+        const uint8_t* src = side ? r : l;
+        uint8_t* pin = w->h_in + ((size_t)side * K + j) * img;
+        if (step == rowb) std::memcpy(pin, src, img);
+        else for (int y = 0; y < rows; ++y) std::memcpy(pin + y * rowb, src + y * step, rowb);
+        uint8_t* dst = (side ? w->in_right : w->in_left) + (size_t)j * w->in_cap;
+        HIP_OK(hipMemcpyAsync(dst, pin, img, hipMemcpyHostToDevice, w->stream));
+        (side ? in.right[j] : in.left[j]) = dst;
     }
     return TSM_OK;
 }
@@ -1026,21 +1045,12 @@ int tsm_adc_compute_batch(tsm_adc* h, int n, const uint8_t* const* ls, const uin
         if ((rc = wait_previous_group(h, g, nws)) != TSM_OK) return drain_after_error(h, rc);
         PairIn in{};
         PairOut po{};
-        const size_t rowb = (size_t)cols * 3, img = rowb * rows;
-        for (int j = 0; j < k; ++j) {
-            for (int side = 0; side < 2; ++side) {  // pageable -> pinned (host), pinned -> HBM (async)
-                const uint8_t* src = side ? rs[i0 + j] : ls[i0 + j];
-                uint8_t* pin = w->h_in + ((size_t)side * K + j) * img;
-                if (step == rowb) std::memcpy(pin, src, img);
-                else for (int y = 0; y < rows; ++y) std::memcpy(pin + y * rowb, src + y * step, rowb);
-                uint8_t* dst = (side ? w->in_right : w->in_left) + (size_t)j * w->in_cap;
-                if (hipMemcpyAsync(dst, pin, img, hipMemcpyHostToDevice, w->stream) != hipSuccess)
-                    return drain_after_error(h, fail(h, TSM_ERR_DEVICE, "hipMemcpyAsync (input)"));
-                (side ? in.right[j] : in.left[j]) = dst;
-            }
+        for (int j = 0; j < k; ++j) {  // pageable -> pinned (host), pinned -> HBM (async)
+            if ((rc = stage_pinned_pair(h, w, K, j, ls[i0 + j], rs[i0 + j], rows, cols, step, in)) != TSM_OK)
+                return drain_after_error(h, rc);
             po.out[j] = w->out_dev + (size_t)j * rows * cols;
         }
-        if ((rc = run_pipeline(h, w, k, in, rowb, po, (size_t)cols * 4, nullptr, w->stream)) != TSM_OK)
+        if ((rc = run_pipeline(h, w, k, in, (size_t)cols * 3, po, (size_t)cols * 4, nullptr, w->stream)) != TSM_OK)
             return drain_after_error(h, rc);
         rc = hipMemcpyAsync(w->h_out, w->out_dev, (size_t)k * rows * cols * 4, hipMemcpyDeviceToHost, w->stream) ==
                      hipSuccess ? TSM_OK : TSM_ERR_DEVICE;
