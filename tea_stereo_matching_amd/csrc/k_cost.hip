@@ -233,7 +233,10 @@ __device__ unsigned long long g_stamps[65536 * 8];
 enum { CW_BOTH = 0, CW_VIEW0 = 1, CW_VIEW1 = 2, CW_SHEAR = 3 };
 
 template <int E, bool HSI, bool MASK, int MODE>
-__global__ __launch_bounds__(CW_THREADS) __attribute__((amdgpu_waves_per_eu(E == 3 ? 4 : (E == 4 ? 3 : 1)))) void k_cost_walk(
+#ifndef TSM_CW_WPE3
+#define TSM_CW_WPE3 4  // waves per SIMD asked of the E = 3 walk (measured: 3 -> 209 us, 4 -> 205, 5 / 6 spill: 341 / 384)
+#endif
+__global__ __launch_bounds__(CW_THREADS) __attribute__((amdgpu_waves_per_eu(E == 3 ? TSM_CW_WPE3 : (E == 4 ? 3 : 1)))) void k_cost_walk(
     const uint32_t* __restrict__ desc, const float* __restrict__ lutA, int lutA_n,
     const float* __restrict__ lutB, float* __restrict__ vol, DevParams Pk, int seg_len, int nseg,
     uint32_t* __restrict__ ctr, uint32_t ctr_base) {
