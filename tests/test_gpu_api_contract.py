@@ -173,3 +173,36 @@ def test_batch_host_error_midway_drains_queued_pairs(matcher, tsm):
     # the first two pairs completed before the call returned
     for i in range(2):
         assert np.array_equal(outs[i], matcher.compute(*pairs[i]))
+
+
+def test_host_paths_with_padded_row_steps(matcher, tsm):
+    """Host images and outputs with row steps wider than the row (cv::Mat ROIs): the
+    pinned staging copies row by row, through the single call and a batch of groups that
+    reuse a workspace (5 pairs in groups of 2 over two workspaces)."""
+    from tea_stereo_matching_amd import _native as N
+
+    H, W, pad_in, pad_out = 36, 70, 13, 5
+    pairs = [tsm.synthetic.make_scene(400 + i, H, W, 17)[:2] for i in range(5)]
+    matcher.setMatchingStrategy(tsm.ColorModel.RGB)
+    matcher.setMinMaxDisparity(0, 16)
+    matcher.setConcurrency(2)
+    want = [matcher.compute(l, r) for l, r in pairs]
+    step, ostep = W * 3 + pad_in, W * 4 + 4 * pad_out
+    bl = [np.zeros((H, step), np.uint8) for _ in pairs]
+    br = [np.zeros((H, step), np.uint8) for _ in pairs]
+    for i, (l, r) in enumerate(pairs):
+        bl[i][:, :W * 3] = l.reshape(H, W * 3)
+        br[i][:, :W * 3] = r.reshape(H, W * 3)
+    outs = [np.full((H, W + pad_out), -7.0, np.float32) for _ in pairs]
+    lib = N.load()
+    lp = (ctypes.c_void_p * 5)(*[x.ctypes.data for x in bl])
+    rp = (ctypes.c_void_p * 5)(*[x.ctypes.data for x in br])
+    op = (ctypes.c_void_p * 5)(*[x.ctypes.data for x in outs])
+    assert lib.tsm_adc_compute_batch(matcher._h, 5, lp, rp, H, W, step, op, ostep) == 0
+    for i in range(5):
+        assert np.array_equal(outs[i][:, :W], want[i])
+        assert np.all(outs[i][:, W:] == -7.0)  # the padding of each output row is untouched
+    one = np.full((H, W + pad_out), -7.0, np.float32)
+    assert lib.tsm_adc_compute(matcher._h, bl[3].ctypes.data, br[3].ctypes.data, H, W, step,
+                               one.ctypes.data, ostep) == 0
+    assert np.array_equal(one[:, :W], want[3]) and np.all(one[:, W:] == -7.0)
