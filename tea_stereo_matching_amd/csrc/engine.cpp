@@ -935,7 +935,6 @@ static int group_plan(tsm_adc* h, int n, int& K, int& nws) {
     return ensure_pool(h, nws);
 }
 
-// Group g's stream waits for group g-1's stagger point (other workspace's stream).
 // Pinned host staging of a group of K pairs (grown, never shrunk).
 static int ensure_pinned(tsm_adc* h, Workspace* w, int rows, int cols, int K) {
     const size_t in_need = (size_t)2 * K * rows * cols * 3, out_need = (size_t)K * rows * cols * 4;
@@ -981,6 +980,7 @@ static int flush_outputs(tsm_adc* h, Workspace* w) {
     return TSM_OK;
 }
 
+// Group g's stream waits for group g-1's stagger point (other workspace's stream).
 static int wait_previous_group(tsm_adc* h, int g, int nws) {
     if (g == 0 || nws < 2 || group_stagger() <= 0) return TSM_OK;
     Workspace* prev = h->ws[(g - 1) % nws];
