@@ -105,8 +105,8 @@ def main():
     B = args.batch
     # synthetic inputs: global pair g uses seed 1000 + g; uploaded once (HBM-resident)
     lefts, rights = [], []
-    for g in Dd.shard(rank, B):
-        l, r, _ = tsm.synthetic.make_scene(Dd.pair_seed(g), H, W, L)
+    seeds = [Dd.pair_seed(g) for g in Dd.shard(rank, B)]
+    for l, r, _ in tsm.synthetic.make_scene_batch(seeds, H, W, L, threads=min(16, os.cpu_count() or 1)):
         lefts.append(torch.from_numpy(l).to(dev))
         rights.append(torch.from_numpy(r).to(dev))
     outs = torch.empty((B, H, W), dtype=torch.float32, device=dev)
@@ -146,6 +146,8 @@ def main():
     m.setProfiling(False)
     stages_conc = m.stageTimes()
     elapsed = Dd.max_over_ranks(elapsed, world, dev)
+    verify = verify_outputs(m, tsm, outs, lefts, rights, seeds, H, W, D)
+    verified = Dd.min_over_ranks(1.0 if verify["ok"] else 0.0, world, dev) == 1.0
 
     # Host-buffer leg (untimed for `value`): the same batch handed over as host (pageable
     # numpy) images and returned to host arrays, i.e. the C ABI's tsm_adc_compute_batch with
@@ -221,6 +223,8 @@ def main():
             "parallelism": f"dp{world} (pairs sharded, RCCL gather to rank 0)" if world > 1 else "dp1",
             "gather": world > 1 and not args.no_gather,
         },
+        "verified": verified,
+        "verification": verify["how"] + (" (every rank)" if world > 1 else ""),
         "stage_ms_per_pair": stage_ms,
         "stage_ms_per_pair_in_timed_region": stage_ms_conc,
         "roofline": {
@@ -264,6 +268,32 @@ def main():
         print(json.dumps(line), flush=True)
     if world > 1:
         dist.destroy_process_group()
+
+
+def verify_outputs(m, tsm, outs, lefts, rights, seeds, H, W, D):
+    """After the timed region: the step's outputs are the right ones.  Pair 0 of this rank
+    against the oracle's SHA-256 of its disparity (tests/golden/config_hashes.json, config-B
+    seeds), and the rank's last pair against its own single-frame compute (host API)."""
+    import hashlib
+
+    import numpy as np
+
+    got0 = np.ascontiguousarray(outs[0].cpu().numpy(), dtype=np.float32)
+    how, ok = [], True
+    gold = None
+    try:
+        with open(os.path.join(ROOT, "tests", "golden", "config_hashes.json")) as f:
+            gold = json.load(f).get(f"B_{seeds[0]}")
+    except OSError:
+        pass
+    if gold is not None and (H, W, D) == (375, 1242, 192):
+        ok = ok and hashlib.sha256(got0.tobytes()).hexdigest() == gold["sha256"]
+        how.append(f"pair 0 (seed {seeds[0]}) SHA-256 == oracle's")
+    last = len(seeds) - 1
+    single = m.compute(lefts[last].cpu().numpy(), rights[last].cpu().numpy())
+    ok = ok and bool(np.array_equal(outs[last].cpu().numpy(), single))
+    how.append(f"pair {last} == its single-frame compute()")
+    return {"ok": bool(ok), "how": "; ".join(how)}
 
 
 def hbm_calibration(nbytes, reps=20):

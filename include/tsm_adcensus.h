@@ -146,7 +146,8 @@ int tsm_adc_set_params(tsm_adc* h, const tsm_adc_params* in);
 int tsm_adc_get_disparity_range(const tsm_adc* h, int* min_disparity, int* max_disparity);
 /* Pairs per group in the batch entry points (default 2, at most 64): a group of K pairs
  * runs as one pipeline whose every launch covers the K pairs (K pair slots in one arena),
- * and consecutive groups alternate between two streams. */
+ * and consecutive groups alternate between two streams.  Lowering it releases the HBM of
+ * larger arenas (reallocated for the new group size on next use). */
 int tsm_adc_set_concurrency(tsm_adc* h, int n_streams);
 /* 0/1 (default): serial scanline semantics.  T > 1: reproduce the deterministic
  * lock-step outcome of the reference's racy omp-static scanline schedule on T threads
@@ -159,8 +160,15 @@ int tsm_adc_compute_debug(tsm_adc* h, const uint8_t* left, const uint8_t* right,
 int tsm_adc_set_profiling(tsm_adc* h, int enable);
 int tsm_adc_stage_times(tsm_adc* h, double* ms_sum, int* counts, int n);
 int tsm_adc_reset_stage_times(tsm_adc* h);
-/* Device bytes a workspace needs for a rows x cols pair at the current range. */
+/* Device bytes of ONE pair slot for a rows x cols pair at the current range and colour
+ * model.  A handle holds up to two group arenas of `concurrency` slots each (batches),
+ * plus input / output staging of the same count; single-frame calls use one slot. */
 size_t tsm_adc_workspace_bytes(const tsm_adc* h, int rows, int cols);
+/* bgr2hsi (ADCensus.cpp:1429-1473; filter != 0: the mask / ROI hue-band filter,
+ * :1463-1470) on the device, BGR u8 in, H S I u8 out; synchronous.  The conversion the
+ * HSI model runs before the census (test hook for its bit-exactness). */
+int tsm_adc_convert_hsi(tsm_adc* h, const uint8_t* bgr, int rows, int cols, size_t step, int filter,
+                        uint8_t* out, size_t out_step);
 /* Last error message of the handle ("" if none). */
 const char* tsm_adc_last_error(const tsm_adc* h);
 /* Number of visible HIP devices (0 if none / no runtime). */

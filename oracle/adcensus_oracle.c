@@ -805,6 +805,9 @@ static void bgr2hsi(const uint8_t* src, uint8_t* dst, int H, int W, int filter) 
     }
 }
 
+/* exported for the HSI conversion test (tests/test_gpu_parity.py) */
+void orc_bgr2hsi(const uint8_t* src, uint8_t* dst, int H, int W, int filter) { bgr2hsi(src, dst, H, W, filter); }
+
 static void gauss_median(const uint8_t* src, uint8_t* dst, int H, int W) {
     /* computeGaussMedian, ADCensus.cpp:1475-1499 */
     const size_t n = (size_t)H * W * 3;

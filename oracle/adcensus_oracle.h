@@ -128,6 +128,8 @@ void orc_reproject_3d(const float* disp, int H, int W, size_t step_f, float f, f
                       float cy, float* xyz, size_t out_step_f);
 void orc_reproject_3d_q(const float* disp, int H, int W, size_t step_f, const double* Q,
                         float* xyz, size_t out_step_f);
+/* bgr2hsi, ADCensus.cpp:1429-1473 (filter: the mask / ROI hue band, :1463-1470) */
+void orc_bgr2hsi(const uint8_t* src, uint8_t* dst, int H, int W, int filter);
 void orc_remap_linear_fixed(const uint8_t* src, int sh, int sw, size_t sstep, int C,
                             const int16_t* xy, size_t xy_step_e, const uint16_t* fxy,
                             size_t fxy_step_e, int H, int W, uint8_t* dst, size_t dstep);

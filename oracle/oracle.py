@@ -80,6 +80,7 @@ def lib():
         _lib.orc_reproject_3d.argtypes = [_P, _i, _i, _z, _f, _f, _f, _f, _P, _z]
         _lib.orc_reproject_3d_q.argtypes = [_P, _i, _i, _z, _P, _P, _z]
         _lib.orc_remap_linear_fixed.argtypes = [_P, _i, _i, _z, _i, _P, _z, _P, _z, _i, _i, _P, _z]
+        _lib.orc_bgr2hsi.argtypes = [_P, _P, _i, _i, _i]
         _lib.orc_remap_linear_float.argtypes = [_P, _i, _i, _z, _i, _P, _P, _z, _i, _i, _P, _z]
     return _lib
 
@@ -121,6 +122,14 @@ def compute(left: np.ndarray, right: np.ndarray, params: OrcParams, dump_stages=
     if rc != 0:
         raise RuntimeError(f"orc_compute failed: {rc}")
     return out, dumps
+
+
+def bgr2hsi(img: np.ndarray, filter: int = 0) -> np.ndarray:
+    """bgr2hsi, ADCensus.cpp:1429-1473 ((H, W, 3) BGR -> H S I bytes)."""
+    img = np.ascontiguousarray(img, dtype=np.uint8)
+    out = np.zeros_like(img)
+    lib().orc_bgr2hsi(_ptr(img), _ptr(out), img.shape[0], img.shape[1], int(filter))
+    return out
 
 
 def apply_colormap(disp: np.ndarray) -> np.ndarray:

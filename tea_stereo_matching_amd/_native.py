@@ -83,6 +83,8 @@ SIGNATURES = {
     "tsm_adc_stage_times": (ctypes.c_int, [_P, _P, _P, ctypes.c_int]),
     "tsm_adc_reset_stage_times": (ctypes.c_int, [_P]),
     "tsm_adc_workspace_bytes": (ctypes.c_size_t, [_P, ctypes.c_int, ctypes.c_int]),
+    "tsm_adc_convert_hsi": (ctypes.c_int, [_P, _P, ctypes.c_int, ctypes.c_int, ctypes.c_size_t, ctypes.c_int,
+                                           _P, ctypes.c_size_t]),
     "tsm_adc_last_error": (ctypes.c_char_p, [_P]),
     "tsm_device_count": (ctypes.c_int, []),
     "tsm_version": (ctypes.c_char_p, []),

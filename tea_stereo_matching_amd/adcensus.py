@@ -63,6 +63,7 @@ class ADCensus:
                 "this matcher runs on MI355X only, there is no CPU path")
         self._h = h
         self.device = int(device)
+        self._roi_or_mask = False
 
     # -- lifetime -------------------------------------------------------------
     def close(self) -> None:
@@ -101,6 +102,7 @@ class ADCensus:
                             maskMatching: bool = False) -> None:
         self._ok(self._lib.tsm_adc_set_strategy(self._h, int(colorModel), int(bool(roiMatching)),
                                                 int(bool(maskMatching))))
+        self._roi_or_mask = bool(roiMatching) or bool(maskMatching)
 
     def setOffset(self, offset: int) -> None:
         self._ok(self._lib.tsm_adc_set_offset(self._h, int(offset)))
@@ -191,7 +193,18 @@ class ADCensus:
         self._ok(self._lib.tsm_adc_reset_stage_times(self._h))
 
     def workspaceBytes(self, rows: int, cols: int) -> int:
+        """HBM bytes of one pair slot (a batch handle holds 2 x concurrency of them)."""
         return int(self._lib.tsm_adc_workspace_bytes(self._h, rows, cols))
+
+    def convert_hsi(self, image) -> np.ndarray:
+        """bgr2hsi on the device (ADCensus.cpp:1429-1473) as the current strategy runs it:
+        with the hue-band filter in ROI / mask mode (:1463-1470).  (H, W, 3) H S I bytes."""
+        a = _check_image(image)
+        H, W = a.shape[:2]
+        out = np.empty_like(a)
+        filt = int(self._roi_or_mask)
+        self._ok(self._lib.tsm_adc_convert_hsi(self._h, a.ctypes.data, H, W, W * 3, filt, out.ctypes.data, W * 3))
+        return out
 
     def compute_debug(self, leftImage, rightImage, stages=()) -> tuple[np.ndarray, dict]:
         """compute() plus per-stage dumps in the reference layout (tsm_adc_dump)."""

@@ -15,8 +15,10 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
-#include <string>
 #include <limits>
+#include <mutex>
+#include <string>
+#include <thread>
 #include <vector>
 
 #include "../../include/tsm_adcensus.h"
@@ -118,9 +120,7 @@ struct Workspace {
     uint8_t* gh = nullptr;         // [2][H][gstride]
     RefineBufs rb{};
     // shared by the group's pairs
-    uint32_t* cost_ctr = nullptr;  // cost-walk unit counter (never reset, see k_cost.hip)
     float* infvec = nullptr;       // 64 x +inf (scanline lanes past the label axis)
-    uint32_t cost_ctr_base = 0;
     float* lutA = nullptr;
     float* lutB = nullptr;
     int lutA_n = 0;
@@ -128,8 +128,6 @@ struct Workspace {
     // profiling: per group, its stage events and pair count
     std::vector<hipEvent_t> ev_pool;
     std::vector<std::pair<std::vector<hipEvent_t>, int>> pending;
-    // recorded at the group's stagger point (see group_stagger): the next group starts there
-    hipEvent_t stagger_evt = nullptr;
 };
 
 }  // namespace
@@ -164,14 +162,74 @@ int fail(tsm_adc* h, int code, const std::string& msg) {
             return fail(h, TSM_ERR_DEVICE, std::string(#expr) + ": " + hipGetErrorString(e_)); \
     } while (0)
 
-#ifndef TSM_EXP_LP_ALIGN
-#define TSM_EXP_LP_ALIGN 4
-#endif
-int round_up4(int x) { return (x + TSM_EXP_LP_ALIGN - 1) / TSM_EXP_LP_ALIGN * TSM_EXP_LP_ALIGN; }
+int round_up4(int x) { return (x + 3) / 4 * 4; }
 
-// Supported geometry: the aggregation LDS ring must fit 160 KiB and the per-line
-// kernels hold up to 4 float4 groups per lane.
-constexpr int kMaxLabels = 480;
+// Supported label range: the scanline holds a pixel's label vector in one wave, up to
+// scan_max_lp() labels (8 float4 a lane); every other stage has no label limit.
+int max_labels() { return scan_max_lp(); }
+
+// BGR -> HSI conversion table (bgr2hsi, ADCensus.cpp:1429-1473): entry b | g << 8 | r << 16
+// holds H | S << 8 | I << 16, computed with the reference's float expressions (no
+// contraction: the library builds with -ffp-contract=off) and this host's libm acosf, so
+// the device conversion is a lookup and bit-identical to the host's.  Built once per
+// process (2^24 entries, 64 MiB, threads over the red channel), uploaded once per device.
+const std::vector<uint32_t>& hsi_host_table() {
+    static std::vector<uint32_t> tab;
+    static std::once_flag once;
+    std::call_once(once, [] {
+        tab.resize((size_t)1 << 24);
+        auto fill = [](uint32_t* t, int r0, int r1) {
+            const double tp = 2 * 3.1415926535897932384626433832795;  // 2 * CV_PI
+            for (int ri = r0; ri < r1; ++ri)
+                for (int gi = 0; gi < 256; ++gi)
+                    for (int bi = 0; bi < 256; ++bi) {
+                        const float b = bi / 255.f, g = gi / 255.f, r = ri / 255.f;
+                        const float sum = b + g + r;
+                        const float iv = sum / 3.0f;
+                        const uint32_t I = (uint8_t)(iv * 255);
+                        float sv;
+                        if (sum == 0) sv = 0;
+                        else {
+                            float mn = b < g ? b : g;  // cv::min(cv::min(b, g), r)
+                            mn = mn < r ? mn : r;
+                            sv = 1 - 3 * mn / sum;
+                        }
+                        const uint32_t S = (uint8_t)(sv * 255);
+                        const float den = std::sqrt((r - g) * (r - g) + (r - b) * (g - b));
+                        const float num = (2 * r - g - b) / 2.f;
+                        float hv;
+                        if (den == 0.f || den <= num || sv < 0.05f) hv = 0;
+                        else {
+                            const float theta = std::acos(num / den);  // float overload: acosf
+                            hv = b <= g ? (float)(theta / tp) : (float)(1 - theta / tp);
+                        }
+                        const uint32_t Hh = (uint8_t)(hv * 255);
+                        t[(size_t)bi | ((size_t)gi << 8) | ((size_t)ri << 16)] = Hh | (S << 8) | (I << 16);
+                    }
+        };
+        const int nt = std::max(1, std::min(16, (int)std::thread::hardware_concurrency()));
+        std::vector<std::thread> th;
+        for (int k = 0; k < nt; ++k) th.emplace_back(fill, tab.data(), 256 * k / nt, 256 * (k + 1) / nt);
+        for (auto& t : th) t.join();
+    });
+    return tab;
+}
+
+// The table in HBM of `device` (kept for the process; shared by every handle).
+const uint32_t* hsi_device_table(int device) {
+    static std::mutex mu;
+    static std::vector<uint32_t*> per_dev;
+    std::lock_guard<std::mutex> lk(mu);
+    if ((int)per_dev.size() <= device) per_dev.resize(device + 1, nullptr);
+    if (!per_dev[device]) {
+        const std::vector<uint32_t>& t = hsi_host_table();
+        uint32_t* d = nullptr;
+        if (hipMalloc((void**)&d, t.size() * 4) != hipSuccess) return nullptr;
+        if (hipMemcpy(d, t.data(), t.size() * 4, hipMemcpyHostToDevice) != hipSuccess) { hipFree(d); return nullptr; }
+        per_dev[device] = d;
+    }
+    return per_dev[device];
+}
 
 void free_ws(Workspace* w) {
     for (void* p : w->allocs) hipFree(p);
@@ -223,12 +281,7 @@ void layout_slot(Workspace* w, SlotLayout& S, int H, int W, int L, int model) {
     B.disp1 = B.disp0 + N;
     S.take(B.dm, N * 4);
     S.take(B.dtmp, N * 4);
-    S.take(B.vote, N * 4);
-    S.take(B.samples, N * 20 * 2);
-    S.take(B.flags, N);
-    S.take(B.out_pos, N * 4);
     S.take(B.out_list, N * 4);
-    S.take(B.hi_list, N * 4);
     S.take(B.cvote, N * 4);
     S.take(B.csamp, N * 20 * 2);
     S.take(B.bsum, 2 * refine_scan_blocks((int)N) * 4 + 64);
@@ -247,12 +300,16 @@ void layout_slot(Workspace* w, SlotLayout& S, int H, int W, int L, int model) {
     S.take(B.subpix, N * 4);
 }
 
-size_t workspace_bytes(int H, int W, int L) {
+// Bytes of one pair slot (the per-pair part of a workspace arena), as ensure_workspace
+// lays it out for this range and colour model.
+size_t slot_bytes(int H, int W, int L, int maxD, int model) {
     Workspace tmp;
     SlotLayout S;
-    layout_slot(&tmp, S, H, W, L, TSM_COLOR_HSI);
-    const size_t gs = (size_t)(((W + 2 * grad_pad(L + 255) + 15) / 16) * 16);  // gv, gh (upper bound)
-    return S.off + 2 * (2 * (size_t)H * gs + 256);
+    layout_slot(&tmp, S, H, W, L, model);
+    const size_t gs = (size_t)(((W + 2 * grad_pad(maxD) + 15) / 16) * 16);
+    S.take(tmp.gv, 2 * (size_t)H * gs + 64);
+    S.take(tmp.gh, 2 * (size_t)H * gs + 64);
+    return (S.off + 4095) & ~(size_t)4095;
 }
 
 // Host-built exp tables: the exact float arguments the reference hands to std::exp
@@ -333,13 +390,14 @@ DevParams make_params(const tsm_adc* h, int H, int W) {
 int ensure_workspace(tsm_adc* h, Workspace* w, int H, int W, int K) {
     const int L = h->max_disparity - h->min_disparity + 1;
     if (w->stream == nullptr) HIP_OK(hipStreamCreateWithFlags(&w->stream, hipStreamNonBlocking));
-    if (w->stagger_evt == nullptr) HIP_OK(hipEventCreateWithFlags(&w->stagger_evt, hipEventDisableTiming));
     const tsm_adc_params& p = h->params;
     if (w->H == H && w->W == W && w->L == L && w->maxD == h->max_disparity && w->model == h->color_model &&
         w->lambda_ad == p.lambda_ad && w->lambda_census == p.lambda_census && w->cap >= K)
         return TSM_OK;
     HIP_OK(hipStreamSynchronize(w->stream));
-    const int cap = std::max(K, w->cap);
+    // a geometry / parameter change reallocates anyway: size the arena for the group the
+    // caller needs now (a growing K on the same geometry keeps nothing to preserve either)
+    const int cap = K;
     free_ws(w);
     if (w->in_left) { hipFree(w->in_left); w->in_left = nullptr; }
     if (w->in_right) { hipFree(w->in_right); w->in_right = nullptr; }
@@ -366,7 +424,6 @@ int ensure_workspace(tsm_adc* h, Workspace* w, int H, int W, int K) {
     layout_slot(w, S, H, W, L, h->color_model);
     S.take(w->gv, 2 * (size_t)H * gs + 64);
     S.take(w->gh, 2 * (size_t)H * gs + 64);
-    A(w->cost_ctr, 256);
     A(w->infvec, 256);
     std::vector<float> la, lb;
     build_luts(p, h->color_model, la, lb);
@@ -378,14 +435,12 @@ int ensure_workspace(tsm_adc* h, Workspace* w, int H, int W, int K) {
     HIP_OK(hipMemcpy(w->lutB, lb.data(), lb.size() * 4, hipMemcpyHostToDevice));
     // padded lanes of the volumes are never read as labels; keep the arena defined anyway
     HIP_OK(hipMemset(arena, 0, slot * (size_t)cap));
-    HIP_OK(hipMemset(w->cost_ctr, 0, 256));
     {
         std::vector<float> inf(64, std::numeric_limits<float>::infinity());
         HIP_OK(hipMemcpy(w->infvec, inf.data(), 256, hipMemcpyHostToDevice));
     }
     (void)N;
     (void)Lp;
-    w->cost_ctr_base = 0;
     w->cap = cap;
     w->slot = slot;
     w->H = H;
@@ -424,8 +479,8 @@ int validate(tsm_adc* h, const void* l, const void* r, int rows, int cols, size_
         return fail(h, TSM_ERR_IMAGE, kMsgImage);
     if (h->roi || h->mask) h->max_disparity = cols / 2;  // :339-340 (persists, as in the reference)
     const int L = h->max_disparity - h->min_disparity + 1;
-    if (L <= 1 || L > kMaxLabels)
-        return fail(h, TSM_ERR_UNSUPPORTED, "disparity range of " + std::to_string(L) + " labels is outside [2, " + std::to_string(kMaxLabels) + "]");
+    if (L <= 1 || round_up4(L) > max_labels())
+        return fail(h, TSM_ERR_UNSUPPORTED, "disparity range of " + std::to_string(L) + " labels is outside [2, " + std::to_string(max_labels()) + "]");
     if (h->min_disparity < 0)
         return fail(h, TSM_ERR_UNSUPPORTED, "negative minimum disparity (reference indexes its volume out of bounds, ADCensus.cpp:1398-1404)");
     // build_luts indexes the HSI AD table by 2*hue + 5*(sat + int), exact only for the
@@ -450,20 +505,6 @@ hipEvent_t take_event(Workspace* w) {
     hipEvent_t e;
     hipEventCreate(&e);
     return e;
-}
-
-// Where a batch's next group may start on its own stream (TSM_GROUP_STAGGER): after the
-// cost volume (2), the aggregation (4) or the scanline (5) of the group before it, or at
-// once (0, default).  Measured on config B, batch 64 in groups of 32: lock step 359
-// pairs/s, staggered after the cost 355, after the aggregation 339, after the scanline
-// 342 -- the two groups gain most by filling each other's kernel tails, not by pairing
-// a bandwidth-bound head with a latency-bound tail.
-int group_stagger() {
-    static const int v = [] {
-        const char* e = getenv("TSM_GROUP_STAGGER");
-        return e ? atoi(e) : 0;
-    }();
-    return v;
 }
 
 // Enqueue the full pipeline for a group of K pairs on workspace w (K <= w->cap).
@@ -500,29 +541,20 @@ int run_pipeline(tsm_adc* h, Workspace* w, int K, const PairIn& in, size_t step,
         return TSM_OK;
     };
     int rc;
-    // stagger point: after the stage this many marks in (0 = none)
-    int nmark = 0;
-    const int stagger = group_stagger();
-    auto mark_stage = [&]() {
-        mark();
-        if (stagger > 0 && ++nmark == stagger + 1 && w->stagger_evt) hipEventRecord(w->stagger_evt, st);
-    };
-#ifdef TSM_EXP_SKIP
-    static const int skip = [] { const char* e = getenv("TSM_SKIP"); return e ? atoi(e) : 0; }();
-#else
-    constexpr int skip = 0;
-#endif
+    auto mark_stage = [&]() { mark(); };
 
     mark_stage();
     // --- prep: pack (+HSI), census descriptors -------------------------------------
     launch_pack(in, step, w->img_orig, P, st);
-    if (h->color_model == TSM_COLOR_HSI)
-        launch_hsi(w->img_orig, w->img_tmp, w->img, (h->roi || h->mask) ? 1 : 0, P, st);
+    if (h->color_model == TSM_COLOR_HSI) {
+        const uint32_t* tab = hsi_device_table(h->device);
+        if (!tab) return fail(h, TSM_ERR_OUT_OF_MEMORY, "HSI conversion table");
+        launch_hsi(w->img_orig, w->img_tmp, w->img, (h->roi || h->mask) ? 1 : 0, tab, P, st);
+    }
     launch_census(w->img, w->desc, P, st);
     mark_stage();
     // --- cost volume -------------------------------------------------------------
-    if (!(skip & 16) && launch_cost_volume(w->img, w->desc, w->lutA, w->lutA_n, w->lutB, w->vol, P, w->cost_ctr,
-                           w->cost_ctr_base, st) != 0)
+    if (launch_cost_volume(w->desc, w->lutA, w->lutA_n, w->lutB, w->vol, P, st) != 0)
         return fail(h, TSM_ERR_UNSUPPORTED, "cost volume: label count");
     mark_stage();
     if (dump && dump->images) {
@@ -562,51 +594,34 @@ int run_pipeline(tsm_adc* h, Workspace* w, int K, const PairIn& in, size_t step,
             passes.push_back({hf ? 0 : 1, wsel});
             hf = !hf;
         }
-        // the persistent line streamers (pairs fused) where the geometry fits; the v3 DMA
-        // streamer (one pass per launch) otherwise.  TSM_AGG_KERNEL=dma forces v3.
-        static const int kind = [] {
-            const char* e = getenv("TSM_AGG_KERNEL");
-            return !e ? 0 : e[0] == 'd' ? 1 : 0;
-        }();
-        for (size_t i = 0; i < ((skip & 8) ? 0 : passes.size()); ++i) {
+        // the persistent line streamers fuse each same-direction pass pair into one launch;
+        // arms past their rings run one pass a launch
+        const bool can_fuse = P.max_length1 - 1 <= agg_max_streamer_arm();
+        for (size_t i = 0; i < passes.size(); ++i) {
             const Pass& a = passes[i];
-            const bool pair = i + 1 < passes.size() && a.ws && !passes[i + 1].ws &&
+            const bool pair = can_fuse && i + 1 < passes.size() && a.ws && !passes[i + 1].ws &&
                               passes[i + 1].horizontal == a.horizontal;
-            int rcp = -1;
-            if (kind == 0) {
-                rcp = launch_agg_stream(w->vol, w->arms, a.ws, w->ws, a.horizontal, pair, P, st);
-                if (rcp == 0 && pair) ++i;
-            }
-            if (rcp != 0) rcp = launch_agg_line(w->vol, w->arms, a.ws, a.horizontal, P, st);
-            if (rcp != 0) return fail(h, TSM_ERR_UNSUPPORTED, "aggregation: label count");
+            if (launch_aggregation_pass(w->vol, w->arms, a.ws, w->ws, a.horizontal, pair, P, st) != 0)
+                return fail(h, TSM_ERR_UNSUPPORTED, "aggregation: image too wide for the long-arm pass");
+            if (pair) ++i;
         }
     }
     mark_stage();
     if (dump && dump->cost_agg && (rc = dump_vol(dump->cost_agg, 2)) != TSM_OK) return rc;
     // --- scanline, then WTA of both final volumes --------------------------------------
     const bool keep_view1 = dump && dump->cost_scan;
-    // WTA: fused into the leftward pass (which then never stores view 1's final volume,
-    // only its argmin is used) or, TSM_WTA_FUSED=0, its own launch over both volumes
-    static const bool wta_fused = [] {
-        const char* e = getenv("TSM_WTA_FUSED");
-        return !(e && e[0] == '0');
-    }();
-    bool ok = ((skip & 4) || (launch_scan_vertical(w->vol, w->gv, w->img, +1, w->infvec, P, st) == 0 &&
-              launch_scan_vertical(w->vol, w->gv, w->img, -1, w->infvec, P, st) == 0)) &&
-              ((skip & 2) || launch_scan_horizontal(w->vol, w->gh, w->img, +1, nullptr, 1, w->infvec, P, st) == 0);
-    if (skip & 2) {
-    } else if (ok && wta_fused)
-        ok = launch_scan_horizontal(w->vol, w->gh, w->img, -1, w->rb.disp0, keep_view1 ? 1 : 0, w->infvec, P,
-                                    st) == 0;
-    else if (ok)
-        ok = launch_scan_horizontal(w->vol, w->gh, w->img, -1, nullptr, 1, w->infvec, P, st) == 0 &&
-             launch_wta(w->vol, w->rb.disp0, w->infvec, P, st) == 0;
+    // WTA fused into the leftward pass, which then never stores view 1's final volume
+    // (only its argmin is used) unless a debug dump asks for it
+    const bool ok = launch_scan_vertical(w->vol, w->gv, w->img, +1, w->infvec, P, st) == 0 &&
+                    launch_scan_vertical(w->vol, w->gv, w->img, -1, w->infvec, P, st) == 0 &&
+                    launch_scan_horizontal(w->vol, w->gh, w->img, +1, nullptr, 1, w->infvec, P, st) == 0 &&
+                    launch_scan_horizontal(w->vol, w->gh, w->img, -1, w->rb.disp0, keep_view1 ? 1 : 0,
+                                           w->infvec, P, st) == 0;
     if (!ok) return fail(h, TSM_ERR_UNSUPPORTED, "scanline: label count");
     mark_stage();
     if (keep_view1 && (rc = dump_vol(dump->cost_scan, 2)) != TSM_OK) return rc;
     if (dump && dump->wta && (rc = d2h(dump->wta, w->rb.disp0, 2 * N * 4)) != TSM_OK) return rc;
     // --- refinement --------------------------------------------------------------------
-    if (skip & 1) { mark_stage(); mark_stage(); HIP_OK(hipGetLastError()); if (h->profiling) w->pending.emplace_back(ev, K); return TSM_OK; }
     launch_outlier(w->rb, P, st);
     if (dump && dump->outlier && (rc = d2h(dump->outlier, w->rb.dm, N * 4)) != TSM_OK) return rc;
     {
@@ -732,7 +747,6 @@ int tsm_adc_destroy(tsm_adc* h) {
         for (auto& pe : w->pending) for (hipEvent_t e : pe.first) hipEventDestroy(e);
         for (hipEvent_t e : w->ev_pool) hipEventDestroy(e);
         if (w->stream) hipStreamDestroy(w->stream);
-        if (w->stagger_evt) hipEventDestroy(w->stagger_evt);
         delete w;
     }
     delete h;
@@ -780,8 +794,13 @@ int tsm_adc_get_params(const tsm_adc* h, tsm_adc_params* out) {
 int tsm_adc_set_params(tsm_adc* h, const tsm_adc_params* in) {
     if (!h || !in) return TSM_ERR_ARGUMENT;
     if (in->census_win != 0 && in->census_win != 1) return fail(h, TSM_ERR_ARGUMENT, "census_win must be 0 (9x7) or 1 (7x5)");
-    if (in->max_length1 < 1 || in->max_length1 > 128) return fail(h, TSM_ERR_UNSUPPORTED, "max_length1 outside [1, 128]");
+    // arms are packed as bytes (arm <= maxLength1 - 1 <= 255)
+    if (in->max_length1 < 1 || in->max_length1 > 256) return fail(h, TSM_ERR_UNSUPPORTED, "max_length1 outside [1, 256]");
+    // the refinement keeps at most 20 carried samples per low-vote outlier
     if (in->voting_thresh > 20 || in->voting_thresh < 0) return fail(h, TSM_ERR_UNSUPPORTED, "voting_thresh outside [0, 20]");
+    // colorDiff + 1 is the byte sentinel of the scanline's colour-difference maps
+    if (in->color_diff < 0 || in->color_diff > 254) return fail(h, TSM_ERR_UNSUPPORTED, "color_diff outside [0, 254]");
+    if (in->iterations < 0) return fail(h, TSM_ERR_ARGUMENT, "iterations must be >= 0");
     // k_eq_blur / k_sobel are the fixed 3x3 cv::blur / cv::Canny apertures (ADCensus.cpp:1263-1264)
     if (in->blur_kernel_size != 3) return fail(h, TSM_ERR_UNSUPPORTED, "blur_kernel_size other than 3");
     if (in->canny_kernel_size != 3) return fail(h, TSM_ERR_UNSUPPORTED, "canny_kernel_size other than 3");
@@ -792,6 +811,15 @@ int tsm_adc_set_params(tsm_adc* h, const tsm_adc_params* in) {
 int tsm_adc_set_concurrency(tsm_adc* h, int n) {
     if (!h || n < 1 || n > kMaxGroup) return TSM_ERR_ARGUMENT;
     h->concurrency = n;
+    // a smaller group size gives back the HBM of larger arenas (reallocated on next use)
+    if (set_device(h) != TSM_OK) return TSM_ERR_DEVICE;
+    for (Workspace* w : h->ws) {
+        if (w->cap <= n) continue;
+        if (w->stream && hipStreamSynchronize(w->stream) == hipSuccess) copy_out_pending(w);
+        w->pend_out.clear();
+        collect_profile(h, w);
+        free_ws(w);
+    }
     return TSM_OK;
 }
 
@@ -825,7 +853,7 @@ int tsm_adc_reset_stage_times(tsm_adc* h) {
 size_t tsm_adc_workspace_bytes(const tsm_adc* h, int rows, int cols) {
     if (!h || rows <= 0 || cols <= 0) return 0;
     const int maxd = (h->roi || h->mask) ? cols / 2 : h->max_disparity;
-    return workspace_bytes(rows, cols, maxd - h->min_disparity + 1);
+    return slot_bytes(rows, cols, maxd - h->min_disparity + 1, maxd, h->color_model);
 }
 
 const char* tsm_adc_last_error(const tsm_adc* h) { return h ? h->err.c_str() : "null handle"; }
@@ -911,6 +939,44 @@ static int compute_host(tsm_adc* h, const uint8_t* l, const uint8_t* r, int rows
     return TSM_OK;
 }
 
+int tsm_adc_convert_hsi(tsm_adc* h, const uint8_t* bgr, int rows, int cols, size_t step, int filter,
+                        uint8_t* out, size_t out_step) {
+    if (!h || !bgr || !out || rows <= 0 || cols <= 0 || step < (size_t)cols * 3 || out_step < (size_t)cols * 3)
+        return TSM_ERR_ARGUMENT;
+    int rc;
+    if ((rc = set_device(h)) != TSM_OK) return rc;
+    const uint32_t* tab = hsi_device_table(h->device);
+    if (!tab) return fail(h, TSM_ERR_OUT_OF_MEMORY, "HSI conversion table");
+    const size_t n = (size_t)rows * cols;
+    if (n > (size_t)1 << 30) return fail(h, TSM_ERR_ARGUMENT, "image too large");
+    std::vector<uint32_t> packed(n);
+    for (int y = 0; y < rows; ++y)
+        for (int x = 0; x < cols; ++x) {
+            const uint8_t* s = bgr + (size_t)y * step + (size_t)x * 3;
+            packed[(size_t)y * cols + x] = s[0] | (s[1] << 8) | (s[2] << 16);
+        }
+    uint32_t* d = nullptr;
+    HIP_OK(hipMalloc((void**)&d, 2 * n * 4));
+    hipStream_t st = nullptr;
+    rc = TSM_OK;
+    if (hipMemcpy(d, packed.data(), n * 4, hipMemcpyHostToDevice) != hipSuccess) rc = TSM_ERR_DEVICE;
+    if (rc == TSM_OK) {
+        launch_hsi_convert(d, d + n, (int)n, filter ? 1 : 0, tab, st);
+        if (hipMemcpy(packed.data(), d + n, n * 4, hipMemcpyDeviceToHost) != hipSuccess) rc = TSM_ERR_DEVICE;
+    }
+    hipFree(d);
+    if (rc != TSM_OK) return fail(h, rc, "bgr2hsi on the device");
+    for (int y = 0; y < rows; ++y)
+        for (int x = 0; x < cols; ++x) {
+            const uint32_t v = packed[(size_t)y * cols + x];
+            uint8_t* o = out + (size_t)y * out_step + (size_t)x * 3;
+            o[0] = v & 0xff;
+            o[1] = (v >> 8) & 0xff;
+            o[2] = (v >> 16) & 0xff;
+        }
+    return TSM_OK;
+}
+
 int tsm_adc_compute(tsm_adc* h, const uint8_t* l, const uint8_t* r, int rows, int cols, size_t step,
                     float* out, size_t out_step) {
     return compute_host(h, l, r, rows, cols, step, out, out_step, nullptr);
@@ -922,16 +988,13 @@ int tsm_adc_compute_debug(tsm_adc* h, const uint8_t* l, const uint8_t* r, int ro
 }
 
 // Batches run in groups of K = concurrency pairs, alternating between two group
-// workspaces (two streams) when there is more than one group.  K = 1 keeps one
-// workspace: pairs then run strictly one after another (per-stage timing alone).
+// workspaces (two streams) when there is more than one group (three measured no faster:
+// DESIGN §7).  K = 1 keeps one workspace: pairs then run strictly one after another
+// (per-stage timing alone).
 static int group_plan(tsm_adc* h, int n, int& K, int& nws) {
-    static const int streams = [] {  // group workspaces in rotation (tuning: TSM_GROUP_STREAMS)
-        const char* e = getenv("TSM_GROUP_STREAMS");
-        const int v = e ? atoi(e) : 2;
-        return v < 1 ? 1 : (v > 4 ? 4 : v);
-    }();
+    constexpr int kGroupStreams = 2;
     K = std::min(h->concurrency, kMaxGroup);
-    nws = (n > K && K > 1) ? std::min(streams, (n + K - 1) / K) : 1;
+    nws = (n > K && K > 1) ? std::min(kGroupStreams, (n + K - 1) / K) : 1;
     return ensure_pool(h, nws);
 }
 
@@ -980,15 +1043,6 @@ static int flush_outputs(tsm_adc* h, Workspace* w) {
     return TSM_OK;
 }
 
-// Group g's stream waits for group g-1's stagger point (other workspace's stream).
-static int wait_previous_group(tsm_adc* h, int g, int nws) {
-    if (g == 0 || nws < 2 || group_stagger() <= 0) return TSM_OK;
-    Workspace* prev = h->ws[(g - 1) % nws];
-    Workspace* w = h->ws[g % nws];
-    HIP_OK(hipStreamWaitEvent(w->stream, prev->stagger_evt, 0));
-    return TSM_OK;
-}
-
 int tsm_adc_compute_batch_device(tsm_adc* h, int n, const uint8_t* const* dls,
                                  const uint8_t* const* drs, int rows, int cols, size_t step,
                                  float* const* douts, size_t out_step) {
@@ -1005,7 +1059,6 @@ int tsm_adc_compute_batch_device(tsm_adc* h, int n, const uint8_t* const* dls,
         const int k = std::min(K, n - i0);
         Workspace* w = h->ws[g % nws];
         if ((rc = ensure_workspace(h, w, rows, cols, K)) != TSM_OK) return drain_after_error(h, rc);
-        if ((rc = wait_previous_group(h, g, nws)) != TSM_OK) return drain_after_error(h, rc);
         PairIn in{};
         PairOut out{};
         for (int j = 0; j < k; ++j) {
@@ -1042,7 +1095,6 @@ int tsm_adc_compute_batch(tsm_adc* h, int n, const uint8_t* const* ls, const uin
         if ((rc = ensure_input_staging(h, w, rows, (size_t)cols * 3, cols, K)) != TSM_OK)
             return drain_after_error(h, rc);
         if ((rc = ensure_pinned(h, w, rows, cols, K)) != TSM_OK) return drain_after_error(h, rc);
-        if ((rc = wait_previous_group(h, g, nws)) != TSM_OK) return drain_after_error(h, rc);
         PairIn in{};
         PairOut po{};
         for (int j = 0; j < k; ++j) {  // pageable -> pinned (host), pinned -> HBM (async)

@@ -35,25 +35,6 @@ __global__ void k_zero_u32(uint32_t* __restrict__ p, int n, size_t ps) {
 // ---------------------------------------------------------------------------
 // outlier elimination (LR check)
 // ---------------------------------------------------------------------------
-__global__ void k_outlier(const int32_t* __restrict__ dl, const int32_t* __restrict__ dr,
-                          int32_t* __restrict__ out, DevParams Pk) {
-    const DevParams P = Pk;  // kernel args -> registers once (no per-use kernarg reloads)
-    pair_shift(blockIdx.z, P.pstride, dl, dr, out);
-    const int x = blockIdx.x * blockDim.x + threadIdx.x;
-    const int y = blockIdx.y;
-    const int W = P.W;
-    if (x >= W) return;
-    const int32_t* r = dr + (size_t)y * W;
-    int d = dl[(size_t)y * W + x];
-    if (x - d < 0 || iabs_(d - r[x - d]) > P.disp_tolerance) {
-        bool occ = true;
-        for (int k = P.minD; k <= P.maxD; ++k) {
-            if (x - k >= 0 && k == r[x - k]) { occ = false; break; }
-        }
-        d = occ ? -1 : -2; // m_occlusionValue / m_mismatchValue (:415-416)
-    }
-    out[(size_t)y * W + x] = d;
-}
 
 // Row form: the reference's occlusion search (does some k in [minD, maxD] have
 // dR(x - k) == k?) asks whether any right-view pixel c maps onto x (c + dR(c) == x), so
@@ -89,110 +70,8 @@ __device__ __forceinline__ void region_arms(uint32_t a, bool hf, int& oA, int& o
     else { oA = lf; oB = rt; iA = up; iB = dn; }
 }
 
-// Per pixel: vote count of outliers (+ up to 20 samples for low-vote ones) and flags
-// (bit0 outlier, bit1 high-vote).
-__global__ void k_vote_count(const int32_t* __restrict__ disp, int32_t* __restrict__ dtmp,
-                             const uint32_t* __restrict__ arms,
-                             int32_t* __restrict__ vote, uint16_t* __restrict__ samples,
-                             uint8_t* __restrict__ flags, int hf, DevParams Pk) {
-    const DevParams P = Pk;  // kernel args -> registers once (no per-use kernarg reloads)
-    pair_shift(blockIdx.z, P.pstride, disp, dtmp, arms, vote, samples, flags);
-    const int x = blockIdx.x * blockDim.x + threadIdx.x;
-    const int y = blockIdx.y;
-    const int W = P.W;
-    if (x >= W) return;
-    const size_t idx = (size_t)y * W + x;
-    const int minD = P.minD;
-    dtmp[idx] = disp[idx]; // dispTemp starts as the input; k_vote_decide overwrites high-vote outliers
-    if (disp[idx] >= minD) { flags[idx] = 0; vote[idx] = 0; return; }
-    int oA, oB, iA, iB;
-    region_arms(arms[idx], hf, oA, oB, iA, iB);
-    int cnt = 0;
-    uint16_t* smp = samples + idx * kMaxSamples;
-    for (int o = -oA; o <= oB; ++o) {
-        const int yy0 = hf ? y + o : y, xx0 = hf ? x : x + o;
-        int a1, b1, a2, b2;
-        region_arms(arms[(size_t)yy0 * W + xx0], hf, a1, b1, a2, b2);
-        for (int i = -a2; i <= b2; ++i) {
-            const int yy = hf ? y + o : y + i;
-            const int xx = hf ? x + i : x + o;
-            const int dv = disp[(size_t)yy * W + xx];
-            if (dv >= minD) {
-                if (cnt < kMaxSamples) smp[cnt] = (uint16_t)(dv - minD);
-                cnt++;
-            }
-        }
-    }
-    vote[idx] = cnt;
-    flags[idx] = 1 | (cnt > P.voting_thresh ? 2 : 0);
-}
-
-// The same with 16 lanes per pixel (4 pixels of a row per wave): lanes take every 16th
-// outer-arm position, the counts are summed over the group, and only a low-vote outlier
-// (every valid sample kept) walks its region a second time to write the samples at the
-// lanes' prefix positions.  A sample's slot does not matter (k_vote_decide histograms
-// them), only that all of them are kept.
-__global__ __launch_bounds__(256) void k_vote_count_par(const int32_t* __restrict__ disp,
-                                                        int32_t* __restrict__ dtmp,
-                                                        const uint32_t* __restrict__ arms,
-                                                        int32_t* __restrict__ vote,
-                                                        uint16_t* __restrict__ samples,
-                                                        uint8_t* __restrict__ flags, int hf, DevParams Pk) {
-    const DevParams P = Pk;
-    pair_shift(blockIdx.z, P.pstride, disp, dtmp, arms, vote, samples, flags);
-    const int lane = threadIdx.x & 63, sub = lane & 15, base = lane & ~15;
-    const int x = (blockIdx.x * blockDim.x + threadIdx.x) >> 4;
-    const int y = blockIdx.y;
-    const int W = P.W, minD = P.minD;
-    const bool inside = x < W;
-    const size_t idx = (size_t)y * W + (inside ? x : W - 1);
-    const int cur = disp[idx];
-    const bool outlier = inside && cur < minD;
-    if (inside && sub == 0) dtmp[idx] = cur;  // dispTemp starts as the input
-    if (!__any(outlier)) {
-        if (inside && sub == 0) { flags[idx] = 0; vote[idx] = 0; }
-        return;
-    }
-    int oA = 0, oB = -1, iA, iB;
-    if (outlier) region_arms(arms[idx], hf, oA, oB, iA, iB);
-    // walk the outer positions o = -oA + sub + 16 k; `emit` writes the valid samples
-    auto walk = [&](bool emit, int pos, uint16_t* smp) {
-        int cnt = 0;
-        for (int o = -oA + sub; o <= oB; o += 16) {
-            const int yy0 = hf ? y + o : y, xx0 = hf ? x : x + o;
-            int a1, b1, a2, b2;
-            region_arms(arms[(size_t)yy0 * W + xx0], hf, a1, b1, a2, b2);
-            const ptrdiff_t st = hf ? 1 : W;
-            const int32_t* rp = disp + (size_t)yy0 * W + xx0;
-            for (int i = -a2; i <= b2; ++i) {
-                const int dv = rp[(ptrdiff_t)i * st];
-                if (dv >= minD) {
-                    if (emit) smp[pos + cnt] = (uint16_t)(dv - minD);
-                    cnt++;
-                }
-            }
-        }
-        return cnt;
-    };
-    const int mine = outlier ? walk(false, 0, nullptr) : 0;
-    // inclusive prefix over the 16 lanes of the group
-    int incl = mine;
-#pragma unroll
-    for (int d = 1; d < 16; d <<= 1) {
-        const int v = __shfl_up(incl, d, 16);
-        if (sub >= d) incl += v;
-    }
-    const int total = __shfl(incl, base + 15);
-    if (outlier && total <= kMaxSamples && mine > 0) walk(true, incl - mine, samples + idx * kMaxSamples);
-    if (inside && sub == 0) {
-        vote[idx] = outlier ? total : 0;
-        flags[idx] = outlier ? (uint8_t)(1 | (total > P.voting_thresh ? 2 : 0)) : 0;
-    }
-}
-
-// Device-wide exclusive scan of the two flag counters in raster order:
-//   out_pos[p]  = # outliers before p        out_list[out_pos[p]] = p
-//   hi_list[r]  = r-th high-vote outlier      counts = {#outliers, #high-vote}
+// Device-wide exclusive scan of (outliers, high-vote outliers) per block of SC_BLOCK
+// pixels in raster order (k_oscan_count -> k_scan_blocks -> k_oscan_scatter).
 constexpr int SC_THREADS = 256, SC_ITEMS = 16, SC_BLOCK = SC_THREADS * SC_ITEMS;
 
 __device__ __forceinline__ void block_scan2(int& a, int& b, int* sa, int* sb) {
@@ -214,21 +93,6 @@ __device__ __forceinline__ void block_scan2(int& a, int& b, int* sa, int* sb) {
     b = ib - b;
 }
 
-__global__ void k_scan_count(const uint8_t* __restrict__ flags, int n, int32_t* __restrict__ bsum, size_t ps) {
-    pair_shift(blockIdx.z, ps, flags, bsum);
-    __shared__ int sa[SC_THREADS], sb[SC_THREADS];
-    const int base = blockIdx.x * SC_BLOCK + threadIdx.x * SC_ITEMS;
-    int a = 0, b = 0;
-    for (int k = 0; k < SC_ITEMS; ++k) {
-        const int p = base + k;
-        if (p < n) { const uint8_t f = flags[p]; a += f & 1; b += (f >> 1) & 1; }
-    }
-    block_scan2(a, b, sa, sb);
-    if (threadIdx.x == SC_THREADS - 1) {
-        bsum[2 * blockIdx.x] = sa[SC_THREADS - 1];
-        bsum[2 * blockIdx.x + 1] = sb[SC_THREADS - 1];
-    }
-}
 
 __global__ void k_scan_blocks(int32_t* __restrict__ bsum, int nb, int32_t* __restrict__ counts, size_t ps) {
     pair_shift(blockIdx.z, ps, bsum, counts);
@@ -252,130 +116,14 @@ __global__ void k_scan_blocks(int32_t* __restrict__ bsum, int nb, int32_t* __res
     if (threadIdx.x == SC_THREADS - 1) { counts[0] = sa[SC_THREADS - 1]; counts[1] = sb[SC_THREADS - 1]; }
 }
 
-__global__ void k_scan_scatter(const uint8_t* __restrict__ flags, int n,
-                               const int32_t* __restrict__ bsum, int32_t* __restrict__ out_pos,
-                               int32_t* __restrict__ out_list, int32_t* __restrict__ hi_list, size_t ps) {
-    pair_shift(blockIdx.z, ps, flags, bsum, out_pos, out_list, hi_list);
-    __shared__ int sa[SC_THREADS], sb[SC_THREADS];
-    const int base = blockIdx.x * SC_BLOCK + threadIdx.x * SC_ITEMS;
-    int a = 0, b = 0;
-    for (int k = 0; k < SC_ITEMS; ++k) {
-        const int p = base + k;
-        if (p < n) { const uint8_t f = flags[p]; a += f & 1; b += (f >> 1) & 1; }
-    }
-    block_scan2(a, b, sa, sb);
-    a += bsum[2 * blockIdx.x];
-    b += bsum[2 * blockIdx.x + 1];
-    for (int k = 0; k < SC_ITEMS; ++k) {
-        const int p = base + k;
-        if (p >= n) break;
-        const uint8_t f = flags[p];
-        if (f & 1) { out_pos[p] = a; out_list[a] = p; a++; }
-        if (f & 2) { hi_list[b] = p; b++; }
-    }
-}
-
-// The outliers' votes and low-vote samples laid out by outlier rank, so a high-vote
-// outlier's carry range is one contiguous run for k_vote_decide (thread per rank, the
-// 40-B sample record moved as ten dwords).
-__global__ void k_rank_samples(const int32_t* __restrict__ out_list, const int32_t* __restrict__ counts,
-                               const int32_t* __restrict__ vote, const uint16_t* __restrict__ samples,
-                               int32_t* __restrict__ cvote, uint16_t* __restrict__ csamp, size_t ps) {
-    pair_shift(blockIdx.z, ps, out_list, counts, vote, samples, cvote, csamp);
-    const int a = blockIdx.x * blockDim.x + threadIdx.x;
-    if (a >= counts[0]) return;
-    const int p = out_list[a];
-    const int c = vote[p];
-    cvote[a] = c;
-    if (c > kMaxSamples) return;  // high-vote: never carried
-    const uint32_t* src = reinterpret_cast<const uint32_t*>(samples + (size_t)p * kMaxSamples);
-    uint32_t* dst = reinterpret_cast<uint32_t*>(csamp + (size_t)a * kMaxSamples);
-#pragma unroll
-    for (int i = 0; i < kMaxSamples / 2; ++i) dst[i] = src[i];
-}
 
 // One wave per high-vote outlier: LDS histogram of its own region + carried samples,
 // then the first argmax and the ratio test (:1137-1153).
 constexpr int VD_THREADS = 256;
 
-__global__ __launch_bounds__(VD_THREADS) void k_vote_decide(
-    const int32_t* __restrict__ disp, int32_t* __restrict__ dtmp, const uint32_t* __restrict__ arms,
-    const int32_t* __restrict__ vote, const uint16_t* __restrict__ samples,
-    const int32_t* __restrict__ out_pos, const int32_t* __restrict__ cvote,
-    const uint16_t* __restrict__ csamp,
-    const int32_t* __restrict__ hi_list, const int32_t* __restrict__ counts, int hf, DevParams Pk) {
-    const DevParams P = Pk;  // kernel args -> registers once (no per-use kernarg reloads)
-    pair_shift(blockIdx.z, P.pstride, disp, dtmp, arms, vote, samples, out_pos, cvote, csamp, hi_list, counts);
-    extern __shared__ int hist_all[];
-    const int L = P.L, W = P.W, minD = P.minD;
-    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    int* hist = hist_all + wave * L;
-    const int nhi = counts[1];
-    const int nwaves = gridDim.x * (VD_THREADS / 64);
-    for (int r = blockIdx.x * (VD_THREADS / 64) + wave; r < nhi; r += nwaves) {
-        for (int d = lane; d < L; d += 64) hist[d] = 0;
-        __builtin_amdgcn_wave_barrier();
-        const int p = hi_list[r];
-        const int y = p / W, x = p - y * W;
-        int oA, oB, iA, iB;
-        region_arms(arms[p], hf, oA, oB, iA, iB);
-        for (int o = -oA + lane; o <= oB; o += 64) {
-            const int yy0 = hf ? y + o : y, xx0 = hf ? x : x + o;
-            int a1, b1, a2, b2;
-            region_arms(arms[(size_t)yy0 * W + xx0], hf, a1, b1, a2, b2);
-            // four loads in flight before their histogram adds (the loads are L2 hits on a
-            // dependent chain otherwise); the bins are added in the same order
-            const ptrdiff_t st = hf ? 1 : W;
-            const int32_t* rp = disp + (size_t)yy0 * W + xx0;
-            int i = -a2;
-            for (; i + 3 <= b2; i += 4) {
-                const int d0 = rp[(ptrdiff_t)i * st], d1 = rp[(ptrdiff_t)(i + 1) * st];
-                const int d2 = rp[(ptrdiff_t)(i + 2) * st], d3 = rp[(ptrdiff_t)(i + 3) * st];
-                if (d0 >= minD) atomicAdd(&hist[d0 - minD], 1);
-                if (d1 >= minD) atomicAdd(&hist[d1 - minD], 1);
-                if (d2 >= minD) atomicAdd(&hist[d2 - minD], 1);
-                if (d3 >= minD) atomicAdd(&hist[d3 - minD], 1);
-            }
-            for (; i <= b2; ++i) {
-                const int dv = rp[(ptrdiff_t)i * st];
-                if (dv >= minD) atomicAdd(&hist[dv - minD], 1);
-            }
-        }
-        // carried low-vote outliers: (previous high-vote outlier, p) in raster order
-        const int k0 = r > 0 ? out_pos[hi_list[r - 1]] + 1 : 0;
-        const int k1 = out_pos[p];
-        // (rank-ordered copies: consecutive lanes read consecutive 40-B sample records,
-        // one load round trip per entry)
-        for (int k = k0 + lane; k < k1; k += 64) {
-            const int c = cvote[k];
-            const uint32_t* s = reinterpret_cast<const uint32_t*>(csamp + (size_t)k * kMaxSamples);
-            uint32_t wv[kMaxSamples / 2];
-#pragma unroll
-            for (int i = 0; i < kMaxSamples / 2; ++i) wv[i] = s[i];
-#pragma unroll
-            for (int m = 0; m < kMaxSamples; ++m)
-                if (m < c) atomicAdd(&hist[(wv[m >> 1] >> (16 * (m & 1))) & 0xffffu], 1);
-        }
-        __builtin_amdgcn_wave_barrier();
-        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-        // first maximum: key = (~count, d) minimum
-        uint64_t best = ~0ull;
-        for (int d = lane; d < L; d += 64) {
-            const uint64_t key = ((uint64_t)(0xffffffffu - (uint32_t)hist[d]) << 32) | (uint32_t)d;
-            best = key < best ? key : best;
-        }
-        best = wave_min_u64(best);
-        const int cmax = (int)(0xffffffffu - (uint32_t)(best >> 32));
-        const int dbest = (int)(uint32_t)best;
-        const int v = vote[p];
-        const float ratio = cmax / (float)v;
-        if (lane == 0) dtmp[p] = ratio > P.voting_ratio && cmax > 0 ? dbest + minD : disp[p];
-        __builtin_amdgcn_wave_barrier();
-    }
-}
 
 // ---------------------------------------------------------------------------
-// region voting, outlier-list form (the default)
+// region voting, outlier-list form
 // ---------------------------------------------------------------------------
 // The outliers (disp < minD) are ranked in raster order first (one block scan), so the
 // vote count runs on them alone, 16 lanes an outlier, and writes its vote and (for a
@@ -566,49 +314,6 @@ __constant__ int c_ray_w[16] = {0, 2, 2, 2, 0, -2, -2, -2, 1, 2, 2, 1, -1, -2, -
 // The per-ray results are folded as each ray finishes, in ray order, which is exactly
 // the reference's two post-loops (:1211-1216 min for occlusions, :1222-1231 colour-diff
 // selection for mismatches): no per-thread arrays, no dynamic register indexing.
-__global__ void k_interp(const int32_t* __restrict__ disp, int32_t* __restrict__ out,
-                         const uint32_t* __restrict__ img0, DevParams Pk) {
-    const DevParams P = Pk;  // kernel args -> registers once (no per-use kernarg reloads)
-    pair_shift(blockIdx.z, P.pstride, disp, out, img0);
-    const int x = blockIdx.x * blockDim.x + threadIdx.x;
-    const int y = blockIdx.y;
-    const int H = P.H, W = P.W, minD = P.minD;
-    if (x >= W) return;
-    const size_t idx = (size_t)y * W + x;
-    const int cur = disp[idx];
-    if (cur >= minD) { out[idx] = cur; return; }
-    const bool occlusion = cur == minD - 1; // :1209
-    const uint32_t c0 = img0[idx];
-    int res = cur;        // occlusion: running min;  mismatch: md
-    int mdiff = -1;       // mismatch: running mdiff
-    for (int dir = 0; dir < 16; ++dir) {
-        const int sh0 = c_ray_h[dir] / 2, sh1 = c_ray_h[dir] - c_ray_h[dir] / 2;
-        const int sw0 = c_ray_w[dir] / 2, sw1 = c_ray_w[dir] - c_ray_w[dir] / 2;
-        int nd = cur, ndiff = -1;
-        int hD = y, wD = x;
-        for (int s = 0; s < P.max_search_depth; ++s) {
-            hD += (s & 1) ? sh1 : sh0;
-            wD += (s & 1) ? sw1 : sw0;
-            if (hD < 0 || hD >= H || wD < 0 || wD >= W) break;
-            const int dv = disp[(size_t)hD * W + wD];
-            if (dv >= minD) {
-                nd = dv;
-                ndiff = color_diff(P, c0, img0[(size_t)hD * W + wD]);
-                break;
-            }
-        }
-        if (occlusion) {
-            res = dir == 0 ? nd : min(res, nd);
-        } else if (dir == 0) {
-            res = nd;
-            mdiff = ndiff;
-        } else if (mdiff < 0 || (mdiff > ndiff && ndiff > 0)) {
-            res = nd;
-            mdiff = ndiff;
-        }
-    }
-    out[idx] = res;
-}
 
 // Ray-parallel form: 16 lanes per pixel, lane = ray, 4 pixels of a row per wave.  The
 // rays' dependent load chains (<= max_search_depth steps each) run side by side instead
@@ -822,31 +527,11 @@ __device__ __forceinline__ void uf_union(int* parent, int a, int b) {
     }
 }
 
-__global__ void k_uf_init(const uint8_t* __restrict__ map, int32_t* __restrict__ label, int n, size_t ps) {
-    pair_shift(blockIdx.z, ps, map, label);
-    const int i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i < n) label[i] = map[i] != 1 ? i : -1;
-}
 
-__global__ void k_uf_merge(const uint8_t* __restrict__ map, int32_t* __restrict__ label, int H, int W, size_t ps) {
-    pair_shift(blockIdx.z, ps, map, label);
-    const int x = blockIdx.x * blockDim.x + threadIdx.x;
-    const int y = blockIdx.y;
-    if (x >= W) return;
-    const int i = y * W + x;
-    if (map[i] == 1) return;
-    // W, NW, N, NE neighbours cover every 8-connected edge once
-    if (x > 0 && map[i - 1] != 1) uf_union(label, i, i - 1);
-    if (y > 0) {
-        if (x > 0 && map[i - W - 1] != 1) uf_union(label, i, i - W - 1);
-        if (map[i - W] != 1) uf_union(label, i, i - W);
-        if (x + 1 < W && map[i - W + 1] != 1) uf_union(label, i, i - W + 1);
-    }
-}
 
 // Tiled form: union-find inside a 32x32 tile in LDS (LDS atomics), global labels are
 // the tile roots' pixel indices; then only the pairs crossing a tile edge merge in global
-// memory.  Same components as k_uf_merge.
+// memory.
 constexpr int UT = 32;
 
 __device__ __forceinline__ int lds_find(int* lab, int x) {
@@ -1072,14 +757,7 @@ static dim3 grid2d(int W, int H, int bx, const DevParams& P) { return dim3((W + 
 static dim3 grid1d(size_t n, const DevParams& P) { return dim3((unsigned)n, 1, P.npairs); }
 
 void launch_outlier(RefineBufs& B, const DevParams& P, hipStream_t st) {
-    static const bool serial = [] {
-        const char* e = getenv("TSM_OUTLIER_SERIAL");  // A/B: the per-pixel disparity search
-        return e && e[0] == '1';
-    }();
-    if (serial)
-        hipLaunchKernelGGL(k_outlier, grid2d(P.W, P.H, 256, P), dim3(256), 0, st, B.disp0, B.disp1, B.dm, P);
-    else
-        hipLaunchKernelGGL(k_outlier_row, grid1d(P.H, P), dim3(256), (size_t)P.W, st, B.disp0, B.disp1, B.dm, P);
+    hipLaunchKernelGGL(k_outlier_row, grid1d(P.H, P), dim3(256), (size_t)P.W, st, B.disp0, B.disp1, B.dm, P);
     trace_point("k_outlier", st);
 }
 
@@ -1089,66 +767,29 @@ void launch_region_voting(RefineBufs& B, const uint32_t* arms0, int hf, const De
     const int n = P.H * P.W;
     const int nb = (int)refine_scan_blocks(n);
     const size_t ps = P.pstride;
-    static const bool old_flow = [] {
-        const char* e = getenv("TSM_VOTE_FLOW");  // A/B: "old" = the per-pixel count + two-counter scan
-        return e && e[0] == 'o';
-    }();
-    if (!old_flow) {
-        hipLaunchKernelGGL(k_oscan_count, grid1d(nb, P), dim3(SC_THREADS), 0, st, B.dm, n, P.minD, B.bsum, ps);
-        trace_point("k_oscan_count", st);
-        hipLaunchKernelGGL(k_scan_blocks, grid1d(1, P), dim3(SC_THREADS), 0, st, B.bsum, nb, B.counts, ps);
-        trace_point("k_scan_blocks", st);
-        hipLaunchKernelGGL(k_oscan_scatter, grid1d(nb, P), dim3(SC_THREADS), 0, st, B.dm, n, P.minD, B.bsum,
-                           B.out_list, B.dtmp, ps);
-        trace_point("k_oscan_scatter", st);
-        // grid-stride over the ranked outliers (their count stays on the device)
-        const int vc_blocks = std::max(64, 1536 / std::max(1, P.npairs));
-        hipLaunchKernelGGL(k_vote_count_rank, grid1d(vc_blocks, P), dim3(256), 0, st, B.dm, arms0, B.out_list,
-                           B.counts, B.cvote, B.csamp, hf, P);
-        trace_point("k_vote_count_rank", st);
-        const size_t lds = (size_t)(VD_THREADS / 64) * P.L * sizeof(int);
-        const int vd_blocks = std::max(128, 1024 / std::max(1, P.npairs));
-        hipLaunchKernelGGL(k_vote_decide_rank, grid1d(vd_blocks, P), dim3(VD_THREADS), lds, st, B.dm, B.dtmp,
-                           arms0, B.out_list, B.cvote, B.csamp, B.counts, hf, P);
-        trace_point("k_vote_decide_rank", st);
-        std::swap(B.dm, B.dtmp);
-        return;
-    }
-    static const bool serial = [] {
-        const char* e = getenv("TSM_VOTE_SERIAL");  // A/B: the one-thread-per-pixel count
-        return e && e[0] == '1';
-    }();
-    if (serial)
-        hipLaunchKernelGGL(k_vote_count, grid2d(P.W, P.H, 128, P), dim3(128), 0, st, B.dm, B.dtmp, arms0,
-                           B.vote, B.samples, B.flags, hf, P);
-    else
-        hipLaunchKernelGGL(k_vote_count_par, grid2d(P.W * 16, P.H, 256, P), dim3(256), 0, st, B.dm, B.dtmp,
-                           arms0, B.vote, B.samples, B.flags, hf, P);
-    trace_point("k_vote_count", st);
-    hipLaunchKernelGGL(k_scan_count, grid1d(nb, P), dim3(SC_THREADS), 0, st, B.flags, n, B.bsum, ps); trace_point("k_scan_count", st);
-    hipLaunchKernelGGL(k_scan_blocks, grid1d(1, P), dim3(SC_THREADS), 0, st, B.bsum, nb, B.counts, ps); trace_point("k_scan_blocks", st);
-    hipLaunchKernelGGL(k_scan_scatter, grid1d(nb, P), dim3(SC_THREADS), 0, st, B.flags, n, B.bsum,
-                       B.out_pos, B.out_list, B.hi_list, ps); trace_point("k_scan_scatter", st);
-    hipLaunchKernelGGL(k_rank_samples, grid1d((n + 255) / 256, P), dim3(256), 0, st, B.out_list, B.counts, B.vote,
-                       B.samples, B.cvote, B.csamp, ps); trace_point("k_rank_samples", st);
+    hipLaunchKernelGGL(k_oscan_count, grid1d(nb, P), dim3(SC_THREADS), 0, st, B.dm, n, P.minD, B.bsum, ps);
+    trace_point("k_oscan_count", st);
+    hipLaunchKernelGGL(k_scan_blocks, grid1d(1, P), dim3(SC_THREADS), 0, st, B.bsum, nb, B.counts, ps);
+    trace_point("k_scan_blocks", st);
+    hipLaunchKernelGGL(k_oscan_scatter, grid1d(nb, P), dim3(SC_THREADS), 0, st, B.dm, n, P.minD, B.bsum,
+                       B.out_list, B.dtmp, ps);
+    trace_point("k_oscan_scatter", st);
+    // grid-stride over the ranked outliers (their count stays on the device)
+    const int vc_blocks = std::max(64, 1536 / std::max(1, P.npairs));
+    hipLaunchKernelGGL(k_vote_count_rank, grid1d(vc_blocks, P), dim3(256), 0, st, B.dm, arms0, B.out_list,
+                       B.counts, B.cvote, B.csamp, hf, P);
+    trace_point("k_vote_count_rank", st);
     const size_t lds = (size_t)(VD_THREADS / 64) * P.L * sizeof(int);
-    // one wave per high-vote outlier (grid-stride); ~4096 waves over the whole group
     const int vd_blocks = std::max(128, 1024 / std::max(1, P.npairs));
-    hipLaunchKernelGGL(k_vote_decide, grid1d(vd_blocks, P), dim3(VD_THREADS), lds, st, B.dm, B.dtmp, arms0,
-                       B.vote, B.samples, B.out_pos, B.cvote, B.csamp, B.hi_list, B.counts, hf, P); trace_point("k_vote_decide", st);
+    hipLaunchKernelGGL(k_vote_decide_rank, grid1d(vd_blocks, P), dim3(VD_THREADS), lds, st, B.dm, B.dtmp,
+                       arms0, B.out_list, B.cvote, B.csamp, B.counts, hf, P);
+    trace_point("k_vote_decide_rank", st);
     std::swap(B.dm, B.dtmp);
 }
 
 void launch_interpolation(RefineBufs& B, const uint32_t* img0, const DevParams& P,
                           hipStream_t st) {
-    static const bool serial = [] {
-        const char* e = getenv("TSM_INTERP_SERIAL");  // A/B: the one-thread-per-pixel form
-        return e && e[0] == '1';
-    }();
-    if (serial)
-        hipLaunchKernelGGL(k_interp, grid2d(P.W, P.H, 128, P), dim3(128), 0, st, B.dm, B.dtmp, img0, P);
-    else
-        hipLaunchKernelGGL(k_interp_rays, grid2d(P.W * 16, P.H, 256, P), dim3(256), 0, st, B.dm, B.dtmp, img0, P);
+    hipLaunchKernelGGL(k_interp_rays, grid2d(P.W * 16, P.H, 256, P), dim3(256), 0, st, B.dm, B.dtmp, img0, P);
     trace_point("k_interp", st);
     std::swap(B.dm, B.dtmp);
 }
@@ -1166,18 +807,9 @@ void launch_discontinuity(RefineBufs& B, const float* vol0, const DevParams& P,
     hipLaunchKernelGGL(k_sobel, grid2d(P.W, P.H, 256, P), dim3(256), 0, st, B.blurred, B.dx, B.dy, B.mag, P.H, P.W, ps); trace_point("k_sobel", st);
     hipLaunchKernelGGL(k_nms, grid2d(P.W, P.H, 256, P), dim3(256), 0, st, B.dx, B.dy, B.mag, B.map,
                        P.H, P.W, P.canny_low, P.canny_high, ps); trace_point("k_nms", st);
-    static const bool flat_uf = [] {
-        const char* e = getenv("TSM_UF_FLAT");  // A/B: global-memory union-find over every pair
-        return e && e[0] == '1';
-    }();
-    if (flat_uf) {
-        hipLaunchKernelGGL(k_uf_init, grid1d((n + 255) / 256, P), dim3(256), 0, st, B.map, B.label, n, ps); trace_point("k_uf_init", st);
-        hipLaunchKernelGGL(k_uf_merge, grid2d(P.W, P.H, 256, P), dim3(256), 0, st, B.map, B.label, P.H, P.W, ps); trace_point("k_uf_merge", st);
-    } else {
-        hipLaunchKernelGGL(k_uf_tile, dim3((P.W + UT - 1) / UT, (P.H + UT - 1) / UT, P.npairs), dim3(256), 0, st, B.map,
-                           B.label, P.H, P.W, ps); trace_point("k_uf_tile", st);
-        hipLaunchKernelGGL(k_uf_edges, grid2d(P.W, P.H, 256, P), dim3(256), 0, st, B.map, B.label, P.H, P.W, ps); trace_point("k_uf_edges", st);
-    }
+    hipLaunchKernelGGL(k_uf_tile, dim3((P.W + UT - 1) / UT, (P.H + UT - 1) / UT, P.npairs), dim3(256), 0, st, B.map,
+                       B.label, P.H, P.W, ps); trace_point("k_uf_tile", st);
+    hipLaunchKernelGGL(k_uf_edges, grid2d(P.W, P.H, 256, P), dim3(256), 0, st, B.map, B.label, P.H, P.W, ps); trace_point("k_uf_edges", st);
     hipLaunchKernelGGL(k_zero_u32, grid1d((n / 4 + 256) / 256, P), dim3(256), 0, st, reinterpret_cast<uint32_t*>(B.strong), (n + 3) / 4, ps); trace_point("k_zero_u32", st);
     hipLaunchKernelGGL(k_uf_flatten_mark, grid1d((n + 255) / 256, P), dim3(256), 0, st, B.map, B.label, B.strong, n, ps); trace_point("k_uf_flatten_mark", st);
     hipLaunchKernelGGL(k_uf_final, grid1d((n + 255) / 256, P), dim3(256), 0, st, B.map, B.label, B.strong, B.edges, n, ps); trace_point("k_uf_final", st);

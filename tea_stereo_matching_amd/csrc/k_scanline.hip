@@ -167,7 +167,7 @@ struct LaneAddr {
 };
 
 // Buffer resources of the byte maps / image; offsets are 32-bit (checked by the launcher).
-constexpr int SC_GBIAS = 512;  // >= 4 * (max label vectors = 128): no negative buffer offset
+constexpr int SC_GBIAS = 2048;  // >= 4 * (max label vectors = 512): no negative buffer offset
 
 struct ScanRes {
     __amdgpu_buffer_rsrc_t own;   // own-view colour differences (d1)
@@ -183,7 +183,7 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t scan_rsrc(const void* p) {
 // scalar (uniform) plus, for d2, a per-lane constant: no per-step address arithmetic.
 //   d2 window of lane q: aligned byte (x0 + gb) & ~3 = S + V with S = (x0 [- 3]) & ~3
 //   (scalar) and V = +4q (view 0) or -4q (view 1); the rsrc sits SC_GBIAS B low so
-//   V + SC_GBIAS >= 0 for every label vector q < 128 (J = 2).
+//   V + SC_GBIAS >= 0 for every label vector q < 512 (J = 8).
 template <int J, bool HORIZ, bool MASK>
 __device__ __forceinline__ void scan_issue(StepIn<J>& s, int pos, int dir, int line,
                                            const float* const (&pv)[J], const uint32_t (&gv)[J],
@@ -268,25 +268,19 @@ __device__ __forceinline__ void partial_opt(f32x4 (&p)[J], const f32x4 (&q)[J], 
 // omp schedule emulation costs two scalar compares per step (chunk starts are tracked
 // incrementally).
 // ---------------------------------------------------------------------------
-// Prefetch depth (steps).  Alone, a pass of the horizontal kernel (under one wave per
-// SIMD) is faster with 16 steps in flight; in groups of 32 pairs (24000 waves a launch)
-// 8 steps win (+1 % pairs/s, same-box A/B): 79 instead of 135 VGPRs, 6 instead of 3
-// waves per SIMD.  The vertical passes are HBM-bound at 8.
-#ifndef TSM_SC_KH
-#define TSM_SC_KH 8
-#endif
-#ifndef TSM_SC_KV
-#define TSM_SC_KV 8
-#endif
-template <bool HORIZ> constexpr int sc_k() { return HORIZ ? TSM_SC_KH : TSM_SC_KV; }
-
+// Prefetch depth K (steps), a template parameter.  Alone, a pass of the horizontal kernel
+// (under one wave per SIMD) is faster with 16 steps in flight, so single-pair launches take
+// 16; in groups of pairs (tens of thousands of waves a launch) 8 steps win (+1 % pairs/s,
+// same-box A/B): 79 instead of 135 VGPRs, 6 instead of 3 waves per SIMD.  The vertical
+// passes are HBM-bound at 8.  Wider label vectors (J >= 3) shorten the ring to keep the
+// registers in bounds.
 // first iteration of omp-static chunk t (libgomp / vcomp: first n%T threads take q+1)
 __device__ __forceinline__ int omp_start(int t, int n, int T) {
     const int q = n / T, r = n % T;
     return t * q + (t < r ? t : r);
 }
 
-template <int J, bool HORIZ, bool MASK, bool WTA, bool OMP>
+template <int J, int SC_K, bool HORIZ, bool MASK, bool WTA, bool OMP>
 __global__ __launch_bounds__(256) void k_scan_line(float* __restrict__ vol,
                                                    const uint8_t* __restrict__ grad,
                                                    const uint32_t* __restrict__ img, int dir,
@@ -353,7 +347,6 @@ __global__ __launch_bounds__(256) void k_scan_line(float* __restrict__ vol,
 
     // running per-lane pointers: the prefetch position and the step being written
     // (lanes past the label axis stay on the +inf vector: step 0; storing +inf there is a no-op)
-    constexpr int SC_K = sc_k<HORIZ>();
     const float* pf[J];
     float* cur[J];
     ptrdiff_t dstep[J];
@@ -412,26 +405,15 @@ __global__ __launch_bounds__(256) void k_scan_line(float* __restrict__ vol,
                 if (store && upd) {  // untouched vectors are not rewritten
 #pragma unroll
                     for (int j = 0; j < J; ++j)
-#ifdef TSM_EXP_SCAN_NOSTORE
-                        if (q[j].x == -7.f)  // timing experiment only
-#endif
                         st_stream(cur[j], q[j]);
                 }
 #pragma unroll
                 for (int j = 0; j < J; ++j) cur[j] += dstep[j];
-#ifdef TSM_EXP_WTA_LANE0
-                mq = vec_min_bits<J, !WTA>(q);
-                if (WTA) {
-                    const int d = vec_argmin<J>(q, lane, C.L, C.minD, mq);
-                    if (lane == 0) wrow[pos] = d;
-                }
-#else
                 mq = vec_min_bits<J, true>(q);
                 if (WTA) {  // step it's index lands in lane it & 63, stored 64 steps at a time
                     const int d = vec_argmin_nb<J>(q, lane, C.L, C.minD, mq);  // whole wave
                     dacc = lane == (it & 63) ? d : dacc;
                 }
-#endif
                 // refill this slot only now that its data is consumed (a load into a live
                 // slot would make the compiler stage it in temporaries and copy it back,
                 // waiting for the load right away)
@@ -443,38 +425,52 @@ __global__ __launch_bounds__(256) void k_scan_line(float* __restrict__ vol,
                 }
             }
         }
-#ifndef TSM_EXP_WTA_LANE0
         if (WTA && (((b + SC_K) & 63) == 0 || b + SC_K >= n)) {  // flush a group of 64 steps
             const int g0 = b & ~63;
             if (lane < min(n, g0 + 64) - g0) wrow[posbase + dir * (g0 + lane)] = dacc;
         }
-#endif
     }
 }
 
-template <int J, bool HORIZ, bool MASK, bool WTA>
+template <int J, int K, bool HORIZ, bool MASK, bool WTA>
 static void launch_scan_t(float* vol, const uint8_t* grad, const uint32_t* img, int dir, int32_t* wta,
                           int store_view1, const float* infvec, const DevParams& P, hipStream_t st) {
     dim3 g(((HORIZ ? P.H : P.W) + 3) / 4, 2, P.npairs);
     if (P.omp_threads > 1)
-        hipLaunchKernelGGL((k_scan_line<J, HORIZ, MASK, WTA, true>), g, dim3(256), 0, st, vol, grad, img, dir,
+        hipLaunchKernelGGL((k_scan_line<J, K, HORIZ, MASK, WTA, true>), g, dim3(256), 0, st, vol, grad, img, dir,
                            wta, store_view1, infvec, P);
     else
-        hipLaunchKernelGGL((k_scan_line<J, HORIZ, MASK, WTA, false>), g, dim3(256), 0, st, vol, grad, img, dir,
+        hipLaunchKernelGGL((k_scan_line<J, K, HORIZ, MASK, WTA, false>), g, dim3(256), 0, st, vol, grad, img, dir,
                            wta, store_view1, infvec, P);
 }
+
+template <int J, int K, bool HORIZ, bool WTA>
+static void launch_scan_m(float* vol, const uint8_t* grad, const uint32_t* img, int dir, int32_t* wta,
+                          int store_view1, const float* infvec, const DevParams& P, hipStream_t st) {
+    if (P.mask) launch_scan_t<J, K, HORIZ, true, WTA>(vol, grad, img, dir, wta, store_view1, infvec, P, st);
+    else launch_scan_t<J, K, HORIZ, false, WTA>(vol, grad, img, dir, wta, store_view1, infvec, P, st);
+}
+
+// label vectors per lane J = ceil(Lp / 256) (J = 5..8 run as 8, lanes past the axis on +inf)
+int scan_max_lp() { return 8 * 256; }
 
 template <bool HORIZ, bool WTA>
 static int launch_scan(float* vol, const uint8_t* grad, const uint32_t* img, int dir, int32_t* wta,
                        int store_view1, const float* infvec, const DevParams& P, hipStream_t st) {
     const int J = (P.Lp / 4 + 63) / 64;
-    const bool m = P.mask != 0;
+    // a horizontal pass of one or two pairs runs under one wave per SIMD: the deeper ring
+    const bool deep = HORIZ && P.npairs <= 2;
     if (J == 1) {
-        if (m) launch_scan_t<1, HORIZ, true, WTA>(vol, grad, img, dir, wta, store_view1, infvec, P, st);
-        else launch_scan_t<1, HORIZ, false, WTA>(vol, grad, img, dir, wta, store_view1, infvec, P, st);
+        if (deep) launch_scan_m<1, 16, HORIZ, WTA>(vol, grad, img, dir, wta, store_view1, infvec, P, st);
+        else launch_scan_m<1, 8, HORIZ, WTA>(vol, grad, img, dir, wta, store_view1, infvec, P, st);
     } else if (J == 2) {
-        if (m) launch_scan_t<2, HORIZ, true, WTA>(vol, grad, img, dir, wta, store_view1, infvec, P, st);
-        else launch_scan_t<2, HORIZ, false, WTA>(vol, grad, img, dir, wta, store_view1, infvec, P, st);
+        launch_scan_m<2, 8, HORIZ, WTA>(vol, grad, img, dir, wta, store_view1, infvec, P, st);
+    } else if (J == 3) {
+        launch_scan_m<3, 4, HORIZ, WTA>(vol, grad, img, dir, wta, store_view1, infvec, P, st);
+    } else if (J == 4) {
+        launch_scan_m<4, 4, HORIZ, WTA>(vol, grad, img, dir, wta, store_view1, infvec, P, st);
+    } else if (J <= 8) {
+        launch_scan_m<8, 2, HORIZ, WTA>(vol, grad, img, dir, wta, store_view1, infvec, P, st);
     } else {
         return -1;
     }
@@ -492,56 +488,6 @@ int launch_scan_horizontal(float* vol, const uint8_t* gh, const uint32_t* img, i
                            hipStream_t st) {
     if (wta) return launch_scan<true, true>(vol, gh, img, dir, wta, store_view1, infvec, P, st);
     return launch_scan<true, false>(vol, gh, img, dir, nullptr, store_view1, infvec, P, st);
-}
-
-// ---------------------------------------------------------------------------
-// WTA (cost2disparity, ADCensus.cpp:1394-1413) over the final volumes of both views,
-// as its own memory-bound launch: one wave takes WTA_PX consecutive pixel vectors
-// (views are contiguous: pixel g of [2][H][W] is vector g), all loads in flight first.
-// Keeping the argmin out of the serial leftward pass shortens that pass's chain more
-// than re-reading the volumes costs.
-// ---------------------------------------------------------------------------
-constexpr int WTA_PX = 8;
-
-template <int J>
-__global__ __launch_bounds__(256) void k_wta(const float* __restrict__ vol, int32_t* __restrict__ disp,
-                                             const float* __restrict__ infvec, DevParams Pk) {
-    const DevParams P = Pk;
-    const int lane = threadIdx.x & 63;
-    const size_t npx = (size_t)2 * P.H * P.W;
-    pair_shift(blockIdx.z, P.pstride, vol, disp);
-    const size_t g0 = ((size_t)blockIdx.x * 4 + (threadIdx.x >> 6)) * WTA_PX;
-    if (g0 >= npx) return;
-    const int Q = P.Lp >> 2;
-    f32x4 x[WTA_PX][J];
-#pragma unroll
-    for (int i = 0; i < WTA_PX; ++i) {
-        const size_t g = g0 + i < npx ? g0 + i : npx - 1;
-#pragma unroll
-        for (int j = 0; j < J; ++j) {
-            const int q = lane + 64 * j;
-            x[i][j] = *reinterpret_cast<const f32x4*>(q < Q ? vol + g * P.Lp + 4 * q : infvec);
-        }
-    }
-    int res = 0;
-#pragma unroll
-    for (int i = 0; i < WTA_PX; ++i) {
-        const uint32_t m = vec_min_bits<J>(x[i]);
-        const int d = vec_argmin<J>(x[i], lane, P.L, P.minD, m);
-        res = lane == i ? d : res;
-    }
-    if (lane < WTA_PX && g0 + lane < npx) disp[g0 + lane] = res;
-}
-
-int launch_wta(const float* vol, int32_t* disp, const float* infvec, const DevParams& P, hipStream_t st) {
-    const int J = (P.Lp / 4 + 63) / 64;
-    const size_t npx = (size_t)2 * P.H * P.W;
-    const dim3 g((unsigned)((npx + 4 * WTA_PX - 1) / (4 * WTA_PX)), 1, P.npairs);
-    if (J == 1) hipLaunchKernelGGL((k_wta<1>), g, dim3(256), 0, st, vol, disp, infvec, P);
-    else if (J == 2) hipLaunchKernelGGL((k_wta<2>), g, dim3(256), 0, st, vol, disp, infvec, P);
-    else return -1;
-    trace_point("k_wta", st);
-    return 0;
 }
 
 }  // namespace tsm

@@ -58,11 +58,7 @@ struct DevParams {
 // before it has left the caches anyway.  Measured on the aggregation streamer: -6.6 %
 // per launch against plain stores (nt LOADS measured slower and are not used).
 __device__ __forceinline__ void st_stream(float* p, f32x4 v) {
-#ifdef TSM_EXP_PLAIN_STORES
-    *reinterpret_cast<f32x4*>(p) = v;
-#else
     __builtin_nontemporal_store(v, reinterpret_cast<f32x4*>(p));
-#endif
 }
 
 // Largest group a launch carries (pointer tables of per-pair user buffers are kernel

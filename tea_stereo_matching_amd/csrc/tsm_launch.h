@@ -15,27 +15,28 @@ void trace_point(const char* what, hipStream_t st);
 // k_cost.hip
 // Every launcher runs its stage for the group's P.npairs pairs (DevParams.pstride apart).
 void launch_pack(const PairIn& in, size_t step, uint32_t* img, const DevParams& P, hipStream_t st);
-void launch_hsi(const uint32_t* src, uint32_t* tmp, uint32_t* dst, int filter, const DevParams& P,
-                hipStream_t st);
+// table: the 2^24-entry BGR -> HSI table (engine.cpp hsi_table)
+void launch_hsi(const uint32_t* src, uint32_t* tmp, uint32_t* dst, int filter, const uint32_t* table,
+                const DevParams& P, hipStream_t st);
+// n packed pixels through bgr2hsi alone (tsm_adc_convert_hsi)
+void launch_hsi_convert(const uint32_t* src, uint32_t* dst, int n, int filter, const uint32_t* table, hipStream_t st);
 void launch_census(const uint32_t* img, uint32_t* desc, const DevParams& P, hipStream_t st);
-size_t cost_volume_lds_bytes(const DevParams& P, int lutA_n);
-// ctr: a device word owned by the workspace; ctr_base: its host-side launch offset,
-// advanced by the call (the counter is never reset between launches)
-int launch_cost_volume(const uint32_t* img, const uint32_t* desc, const float* lutA, int lutA_n,
-                       const float* lutB, float* vol, const DevParams& P, uint32_t* ctr,
-                       uint32_t& ctr_base, hipStream_t st);
+size_t cost_volume_lds_bytes(const DevParams& P);
+int launch_cost_volume(const uint32_t* desc, const float* lutA, int lutA_n, const float* lutB, float* vol,
+                       const DevParams& P, hipStream_t st);
 
 // k_aggregate.hip
 void launch_arms(const uint32_t* img, uint32_t* arms, const DevParams& P, hipStream_t st);
 void launch_window_sizes(const uint32_t* arms, int32_t* ws, const DevParams& P, hipStream_t st);
 void launch_color_grad(const uint32_t* img, uint8_t* gv, uint8_t* gh, const DevParams& P,
                        hipStream_t st);
-size_t agg_lds_bytes(const DevParams& P);
-// ws_base: the window-size workspace (ws, reciprocals, packed descriptors; k_window_sizes)
-int launch_agg_stream(float* vol, const uint32_t* arms, const int32_t* ws, const int32_t* ws_base,
-                      int horizontal, bool fused, const DevParams& P, hipStream_t st);
-int launch_agg_line(float* vol, const uint32_t* arms, const int32_t* ws, int horizontal,
-                    const DevParams& P, hipStream_t st);
+// One 1-D aggregation pass (fused: this pass and the next same-direction one) in place.
+// ws: window sizes of a dividing pass (nullptr: no divide); ws_base: the window-size
+// workspace (reciprocals, packed descriptors; k_window_sizes).  Arms longer than
+// agg_max_streamer_arm() run one pass a launch (fused returns -1).  Returns 0 or -1.
+int agg_max_streamer_arm();
+int launch_aggregation_pass(float* vol, const uint32_t* arms, const int32_t* ws, const int32_t* ws_base,
+                            int horizontal, bool fused, const DevParams& P, hipStream_t st);
 
 // k_scanline.hip
 // infvec: >= 16 bytes of +inf (the vector lanes past the label axis read)
@@ -44,8 +45,8 @@ int launch_scan_vertical(float* vol, const uint8_t* gv, const uint32_t* img, int
 int launch_scan_horizontal(float* vol, const uint8_t* gh, const uint32_t* img, int dir,
                            int32_t* wta, int store_view1, const float* infvec, const DevParams& P,
                            hipStream_t st);
-// WTA of both views' final volumes into wta[2][H][W]
-int launch_wta(const float* vol, int32_t* wta, const float* infvec, const DevParams& P, hipStream_t st);
+// largest padded label count the scanline handles (label vectors a lane)
+int scan_max_lp();
 
 // k_refine.hip
 struct RefineBufs {
@@ -53,12 +54,7 @@ struct RefineBufs {
     int32_t* disp1;   // WTA view 1           [H][W]
     int32_t* dm;      // working disparity    [H][W]
     int32_t* dtmp;    // Jacobi scratch       [H][W]
-    int32_t* vote;    // per-pixel vote count [H][W]
-    uint16_t* samples;// [H][W][20] low-vote samples
-    uint8_t* flags;   // [H][W]
-    int32_t* out_pos; // [H][W]
     int32_t* out_list;// [H][W]
-    int32_t* hi_list; // [H][W]
     int32_t* cvote;   // [H][W] vote count by outlier rank (out_pos order)
     uint16_t* csamp;  // [H][W][20] low-vote samples by outlier rank
     int32_t* bsum;    // scan block sums [2 * nblocks]

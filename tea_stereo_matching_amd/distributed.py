@@ -51,3 +51,15 @@ def max_over_ranks(value: float, world: int, device=None) -> float:
     t = torch.tensor([value], dtype=torch.float64, device=device)
     dist.all_reduce(t, op=dist.ReduceOp.MAX)
     return float(t.item())
+
+
+def min_over_ranks(value: float, world: int, device=None) -> float:
+    """MIN of a float across ranks (e.g. a 1/0 verification flag: every rank must pass)."""
+    if world == 1:
+        return value
+    import torch
+    import torch.distributed as dist
+
+    t = torch.tensor([value], dtype=torch.float64, device=device)
+    dist.all_reduce(t, op=dist.ReduceOp.MIN)
+    return float(t.item())

@@ -116,3 +116,18 @@ def config_c(seed: int = 2000):
 def config_e(seed: int = 3000):
     """2048x1536 grey replicated to BGR, setMinMaxDisparity(0, 320)."""
     return make_scene(seed, 1536, 2048, 321, grayscale=True)
+
+
+def make_scene_batch(seeds, height: int, width: int, num_labels: int, threads: int = 8, **kw):
+    """make_scene(seed, ...) for every seed, generated on a thread pool (numpy releases the
+    GIL): [(left, right, gt), ...] in seed order."""
+    from concurrent.futures import ThreadPoolExecutor
+
+    seeds = list(seeds)
+    with ThreadPoolExecutor(max(1, min(threads, len(seeds)))) as ex:
+        return list(ex.map(lambda s: make_scene(s, height, width, num_labels, **kw), seeds))
+
+
+def config_b_batch(seeds, threads: int = 8):
+    """config_b(seed) for every seed (make_scene_batch)."""
+    return make_scene_batch(seeds, 375, 1242, 193, threads)

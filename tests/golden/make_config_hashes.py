@@ -1,15 +1,27 @@
 #!/usr/bin/env python3
-"""Golden hashes for SURVEY §8 configs C and E at full size (test infrastructure).
+"""Golden hashes for SURVEY §8 configs at full size (test infrastructure).
 
-Runs the oracle (oracle/, the C restatement of source/ADCensus.cpp) on the synthetic
-config C pair (1500x1000, setMinMaxDisparity(0, 256)), config E pair (2048x1536 grey
-replicated to BGR, setMinMaxDisparity(0, 320)) and a 2400x1600 pair at D=[0,192] (a volume
-past 2 GiB at config B's label count), serial scanline semantics, RGB model,
-and records the SHA-256 of the fp32 disparity bytes plus a few statistics in
-tests/golden/config_hashes.json.  The GPU test compares its own output's hash: a
-bit-exact check at sizes whose oracle run takes minutes (too long for the GPU suite).
+Runs the oracle (oracle/, the C restatement of source/ADCensus.cpp) with serial scanline
+semantics and records the SHA-256 of the fp32 disparity bytes plus a few statistics in
+tests/golden/config_hashes.json.  The GPU tests (and bench.py's output check) compare
+their own output's hash: a bit-exact check at sizes whose oracle run takes seconds to
+minutes (too long for the GPU suite).
 
-    python tests/golden/make_config_hashes.py [--threads N]
+Cases:
+  C       synthetic config C pair (1500x1000, setMinMaxDisparity(0, 256)), RGB
+  E       synthetic config E pair (2048x1536 grey replicated to BGR, (0, 320)), RGB
+  BIG49   2400x1600 at D=[0,192]: a volume past 2 GiB at config B's label count
+  B_<s>   synthetic config B pair of seed s (1242x375, (0, 192)), RGB: the benchmark's
+          own pairs -- group boundaries of the 128-pair / 64-per-group batch and the
+          first pair of every rank of an 8-GPU run (bench.py checks its pair 0)
+  MOTO    the reference's demo-imgs/Motorcycle_Left/Right.png (1482x994, the real
+          Middlebury pair of config C), setMinMaxDisparity(0, 256), RGB
+  ROI_0600       demo-imgs/0600 (1280x720) with roiMatching, RGB: maxD := W/2 = 640
+                 (ADCensus.cpp:339-340), 641 labels
+  MASK_HSI_0600  the same pair with maskMatching in the reference's default HSI model
+                 (bgr2hsi with the hue-band filter blacks out the background, :1463-1470)
+
+    python tests/golden/make_config_hashes.py [--threads N] [--only C B_1000 ...]
 """
 import argparse
 import hashlib
@@ -26,34 +38,67 @@ sys.path.insert(0, ROOT)
 import tea_stereo_matching_amd.synthetic as syn  # noqa: E402
 from oracle import oracle as O  # noqa: E402
 
+# config B seeds: batch group edges (64 per group: 1063 | 1064, 1127 | 1128) and the test's
+# partial last group (1149), plus the first pair of every bench rank (1000 + 128 r)
+B_SEEDS = sorted({1000, 1063, 1064, 1127, 1149} | {1000 + 128 * r for r in range(8)})
+
+
+def _moto():
+    from PIL import Image
+
+    d = os.path.join(ROOT, "tests", "golden", "demo")
+    ld = lambda n: np.ascontiguousarray(np.array(Image.open(os.path.join(d, n)).convert("RGB"))[:, :, ::-1])  # noqa: E731
+    return ld("Motorcycle_Left.png"), ld("Motorcycle_Right.png"), None
+
+
+def _demo_0600():
+    from PIL import Image
+
+    d = os.path.join(ROOT, "tests", "golden", "demo")
+    ld = lambda n: np.ascontiguousarray(np.array(Image.open(os.path.join(d, n)).convert("RGB"))[:, :, ::-1])  # noqa: E731
+    return ld("0600-Left.png"), ld("0600-Right.png"), None
+
+
+def cases():
+    """(name, pair generator, max_disparity, oracle keyword parameters)"""
+    rgb = {"color_model": O.RGB}
+    out = [("C", syn.config_c, 256, rgb), ("E", syn.config_e, 320, rgb),
+           ("BIG49", lambda: syn.make_scene(4000, 1600, 2400, 193), 192, rgb),
+           ("MOTO", _moto, 256, rgb),
+           ("ROI_0600", _demo_0600, 640, dict(rgb, roi_matching=1)),
+           ("MASK_HSI_0600", _demo_0600, 640, {"color_model": O.HSI, "mask_matching": 1})]
+    for s in B_SEEDS:
+        out.append((f"B_{s}", (lambda s=s: syn.config_b(s)), 192, rgb))
+    return out
+
 
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--threads", type=int, default=os.cpu_count() or 1)
-    ap.add_argument("--only", nargs="*", default=None, help="subset of C, E, BIG49 (others kept)")
+    ap.add_argument("--only", nargs="*", default=None, help="subset of the case names (others kept)")
     args = ap.parse_args()
     path = os.path.join(ROOT, "tests", "golden", "config_hashes.json")
     out = json.load(open(path)) if os.path.exists(path) else {}
-    cases = (("C", syn.config_c, 256), ("E", syn.config_e, 320),
-             # a 6 GB volume at config B's 193 labels: the 64-bit-address aggregation path
-             ("BIG49", lambda: syn.make_scene(4000, 1600, 2400, 193), 192))
-    for name, gen, D in cases:
+    for name, gen, D, kw in cases():
         if args.only and name not in args.only:
             continue
         left, right, _ = gen()
         t0 = time.time()
-        d, _ = O.compute(left, right, O.default_params(O.RGB, 0, D, num_threads=args.threads))
+        kw = dict(kw)
+        model = kw.pop("color_model")
+        d, _ = O.compute(left, right, O.default_params(model, 0, D, num_threads=args.threads, **kw))
         d = np.ascontiguousarray(d, dtype=np.float32)
         out[name] = {
-            "shape": list(d.shape), "max_disparity": D,
+            "shape": list(d.shape), "max_disparity": D, "color_model": model,
+            **{k: v for k, v in kw.items()},
             "sha256": hashlib.sha256(d.tobytes()).hexdigest(),
             "valid_fraction": float((d >= 0).mean()),
             "sum_valid": float(d[d >= 0].astype(np.float64).sum()),
             "oracle_seconds": round(time.time() - t0, 1), "oracle_threads": args.threads,
         }
         print(name, out[name], flush=True)
-    with open(path, "w") as f:
-        json.dump(out, f, indent=1)
+        with open(path, "w") as f:  # after every case: a long run keeps what it has
+            json.dump(out, f, indent=1)
 
 
 if __name__ == "__main__":

@@ -99,6 +99,17 @@ WIDE = [
     (38, 22, 310, 0, 256, 1),
     (39, 20, 300, 0, 258, 0),   # tail float4 with three real labels (257..259)
     (40, 18, 360, 0, 323, 0),   # E = 5 lanes + a full tail (labels 320..323)
+    # every other range setMinMaxDisparity accepts: eight labels a lane (and label slices of
+    # 512 past Lp 512) in the cost walk; the split streamer in as many label slices as keep
+    # its rings inside the CU's LDS; the scanline's 2 / 3 / 4 / 8 label vectors a lane
+    (48, 20, 300, 0, 240, 0),   # Lp 244: four labels a lane, two aggregation slices
+    (41, 16, 300, 0, 264, 0),   # L 265: eight labels a lane
+    (42, 16, 330, 0, 299, 1),   # L 300, HSI
+    (43, 12, 430, 0, 399, 0),   # L 400: two 50-vector aggregation slices
+    (44, 12, 500, 0, 479, 0),   # L 480
+    (45, 10, 700, 0, 640, 0),   # L 641: two cost slices, three scanline vectors a lane
+    (46, 8, 1100, 0, 1024, 0),  # L 1025: three cost slices, eight scanline vectors a lane
+    (47, 12, 430, 7, 330, 1),   # minD > 0 past 256 labels, HSI
 ]
 
 
@@ -252,37 +263,54 @@ def test_default_state_is_reference_default(tsm):
 
 
 def test_hsi_mode_against_oracle(matcher, tsm, oracle):
-    """HSI ("Selective AD-Census-HSI", the reference's default model).  bgr2hsi uses
-    acosf (device libm vs glibc): the converted images may differ in rare hue bytes, so
-    the images are compared with a tolerance and the disparity on >= 99 % of pixels."""
+    """HSI ("Selective AD-Census-HSI", the reference's default model), every stage
+    bit-exact: bgr2hsi's hue byte (acosf, :1456) comes from the host-built conversion table,
+    so the converted images equal the oracle's byte for byte."""
     left, right = _synthetic(tsm, 31, 72, 120, 33)
-    d_g, g = _gpu(matcher, tsm, left, right, 1, 0, 32, ("images",))
-    d_o, o = oracle.compute(left, right, _oracle_params(oracle, oracle.HSI, 0, 32), ("images",))
-    img_diff = np.abs(g["images"].astype(int) - o["images"].astype(int))
-    assert (img_diff <= 1).all()
-    assert (img_diff > 0).mean() < 1e-3
-    if (img_diff == 0).all():
-        assert np.array_equal(d_g, d_o)
-    valid = d_o >= 0
-    assert (np.abs(d_g - d_o)[valid] <= 0.5).mean() >= 0.99
+    d_g, g = _gpu(matcher, tsm, left, right, 1, 0, 32, STAGES)
+    d_o, o = oracle.compute(left, right, _oracle_params(oracle, oracle.HSI, 0, 32), STAGES)
+    _assert_stages_equal(g, o, STAGES)
+    assert np.array_equal(d_g, d_o)
 
 
-@pytest.mark.parametrize("roi,mask", [(True, False), (False, True)])
-def test_roi_mask_modes(matcher, tsm, oracle, roi, mask):
+def test_hsi_conversion_every_colour(matcher, tsm, oracle):
+    """bgr2hsi over all 2^24 BGR colours (a 4096 x 4096 image, each colour once), with and
+    without the mask-mode hue filter: the device table equals the oracle's conversion."""
+    c = np.arange(1 << 24, dtype=np.uint32)
+    img = np.stack([c & 0xff, (c >> 8) & 0xff, c >> 16], -1).astype(np.uint8).reshape(4096, 4096, 3)
+    for mask in (False, True):
+        matcher.setMatchingStrategy(tsm.ColorModel.HSI, False, mask)
+        got = matcher.convert_hsi(img)
+        exp = oracle.bgr2hsi(img, filter=int(mask))
+        if not np.array_equal(got, exp):
+            bad = np.argwhere((got != exp).any(-1))
+            pytest.fail(f"mask={mask}: {len(bad)} colours differ, first BGR {tuple(img[tuple(bad[0])])}: "
+                        f"gpu={tuple(got[tuple(bad[0])])} oracle={tuple(exp[tuple(bad[0])])}")
+    matcher.setMatchingStrategy(tsm.ColorModel.RGB)
+
+
+@pytest.mark.parametrize("roi,mask,model,W", [(True, False, 0, 100), (False, True, 0, 100),
+                                              (True, False, 1, 100), (False, True, 1, 100),
+                                              (False, True, 0, 600), (True, False, 1, 560),
+                                              (True, False, 0, 1300)],
+                         ids=["roi", "mask", "roi_hsi", "mask_hsi", "mask_L301", "roi_hsi_L281", "roi_L651"])
+def test_roi_mask_modes(matcher, tsm, oracle, roi, mask, model, W):
     """ROI / mask matching: maxD := W/2 (:339-340), black pixels excluded from costs,
     arms and scanline (:459-460, :551-555, :625-629, :824, :862), offset and background
     rules on the output (:388-403, :1415-1427)."""
-    left, right = _synthetic(tsm, 41, 64, 100, 51)
+    Hh = 64 if W <= 100 else 12
+    left, right = _synthetic(tsm, 41, Hh, W, min(W // 2 + 1, 120))
     left[:, :12] = 0    # black (masked) band
     right[:, -9:] = 0
     matcher.setOffset(3)
-    d_g, _ = _gpu(matcher, tsm, left, right, 0, 0, 50, roi=roi, mask=mask)
+    d_g, _ = _gpu(matcher, tsm, left, right, model, 0, 50, roi=roi, mask=mask)
     matcher.setOffset(0)
-    p = _oracle_params(oracle, oracle.RGB, 0, 50, roi_matching=int(roi), mask_matching=int(mask),
+    p = _oracle_params(oracle, model, 0, 50, roi_matching=int(roi), mask_matching=int(mask),
                        offset=3)
     d_o, _ = oracle.compute(left, right, p)
     assert np.array_equal(d_g, d_o)
-    assert matcher.getMinMaxDisparity() == (0, 50)  # maxD = W/2 persists (:340)
+    assert matcher.getMinMaxDisparity() == (0, W // 2)  # maxD = W/2 persists (:340)
+    matcher.setMatchingStrategy(tsm.ColorModel.RGB)
 
 
 def test_census_7x5_window(matcher, tsm, oracle):
@@ -322,40 +350,85 @@ def test_full_size_configs_bit_exact(matcher, tsm, cfg):
     assert hashlib.sha256(d_g.tobytes()).hexdigest() == gold["sha256"]
 
 
-MFMA_CHILD = r"""
-import sys
-import numpy as np
-sys.path.insert(0, sys.argv[1])
-import tea_stereo_matching_amd as T
-out = sys.argv[2]
-res = {}
-m = T.ADCensus(0)
-for i, (seed, H, W, mn, mx) in enumerate(((31, 24, 300, 0, 192), (2, 120, 160, 0, 48), (3, 97, 131, 0, 64))):
-    left, right = T.synthetic.make_scene(seed, H, W, mx - mn + 1)[:2]
-    m.setMatchingStrategy(T.ColorModel(0), False, False)
-    m.setMinMaxDisparity(mn, mx)
-    _, g = m.compute_debug(left, right, ("cost_init",))
-    res[f"c{i}"] = g["cost_init"]
-m.close()
-np.savez(out, **res)
-"""
+PARAM_CASES = [
+    # tsm_adc_set_params beyond the defaults (ADCensusParams, stereo_utils.h:209-244):
+    # every field the kernels read, against the oracle, bit-exact
+    ("arms8", 0, dict(max_length1=8, max_length2=4)),
+    ("arms41", 0, dict(max_length1=41, max_length2=20, color_thresh1=40)),   # the streamers' longest arm
+    ("arms60", 0, dict(max_length1=60, max_length2=30, color_thresh1=40)),   # one-pass-a-launch path
+    ("arms128", 1, dict(max_length1=128, max_length2=64, intensity_thresh1=60)),
+    ("iter2", 0, dict(iterations=2)),
+    ("iter6", 1, dict(iterations=6)),
+    ("iter0", 0, dict(iterations=0)),
+    ("p1p2", 0, dict(pi1=0.5, pi2=5.0, color_diff=25)),
+    ("voting", 0, dict(voting_thresh=8, voting_ratio_thresh=0.6, disp_tolerance=1, max_search_depth=7)),
+    ("canny", 1, dict(canny_thresh1=60, canny_thresh2=15, color_thresh2=3)),
+    ("lambdas", 0, dict(lambda_ad=7.5, lambda_census=21.0, census_win=1)),
+]
 
 
-def test_cost_mfma_experiment_bit_exact(oracle, tmp_path):
-    """The opt-in matrix-core cost build (TSM_COST_MFMA=1, an experiment kept beside the
-    popcount walk) produces the oracle's initial volume bit for bit.  The switch is read
-    once per process, so the build runs in a child process."""
-    import subprocess
-    import sys
+@pytest.mark.parametrize("name,model,kw", PARAM_CASES, ids=[c[0] for c in PARAM_CASES])
+def test_params_matrix(matcher, tsm, oracle, name, model, kw):
+    left, right = _synthetic(tsm, 60, 70, 120, 33)
+    matcher.setMatchingStrategy(tsm.ColorModel(model))
+    p = matcher.params()
+    for k, v in kw.items():
+        setattr(p, k, v)
+    matcher.setParams(p)
+    matcher.setMinMaxDisparity(0, 32)
+    matcher.setOmpEmulation(0)
+    d_g, g = matcher.compute_debug(left, right, STAGES)
+    d_o, o = oracle.compute(left, right, _oracle_params(oracle, model, 0, 32, **kw), STAGES)
+    _assert_stages_equal(g, o, STAGES)
+    assert np.array_equal(d_g, d_o)
+    matcher.setMatchingStrategy(tsm.ColorModel.RGB)  # resets the parameter set
 
-    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-    out = str(tmp_path / "mfma.npz")
-    env = dict(os.environ, TSM_COST_MFMA="1")
-    r = subprocess.run([sys.executable, "-c", MFMA_CHILD, root, out], env=env, capture_output=True,
-                       text=True, timeout=120)
-    assert r.returncode == 0, r.stderr[-2000:]
-    got = np.load(out)
-    for i, (seed, H, W, mn, mx) in enumerate(((31, 24, 300, 0, 192), (2, 120, 160, 0, 48), (3, 97, 131, 0, 64))):
-        left, right = _synthetic(__import__("tea_stereo_matching_amd"), seed, H, W, mx - mn + 1)
-        _, o = oracle.compute(left, right, _oracle_params(oracle, oracle.RGB, mn, mx), ("cost_init",))
-        assert np.array_equal(got[f"c{i}"], o["cost_init"]), f"case {i}"
+
+def test_params_refused(matcher, tsm):
+    """What the kernels cannot do exactly is refused, not approximated."""
+    base = matcher.params()
+    for k, v in (("blur_kernel_size", 5), ("canny_kernel_size", 5), ("voting_thresh", 21),
+                 ("max_length1", 257), ("max_length1", 0), ("census_win", 2), ("color_diff", 255),
+                 ("iterations", -1)):
+        p = matcher.params()
+        setattr(p, k, v)
+        with pytest.raises((RuntimeError, tsm.ADCensusError)):
+            matcher.setParams(p)
+        assert getattr(matcher.params(), k) == getattr(base, k)
+
+
+def test_reference_fixture_0045_exact(matcher, tsm, oracle, demo_pair_0045):
+    """Full 1280x720, D=[0,192]: the GPU output at T=20 renders to the reference's own
+    demo-output/0045_ADCensus.png pixel for pixel."""
+    left, right = demo_pair_0045
+    d_g, _ = _gpu(matcher, tsm, left, right, 0, 0, 192, omp=20)
+    ref = load_bgr(os.path.join(GOLDEN, "demo", "0045_ADCensus.png"))
+    col = oracle.apply_colormap(d_g)
+    assert np.array_equal(col, ref), f"{(col != ref).any(-1).sum()} pixels differ"
+
+
+@pytest.mark.parametrize("case", ["MOTO", "ROI_0600", "MASK_HSI_0600"])
+def test_real_pairs_full_size(matcher, tsm, demo_pair_0600, case):
+    """The reference's real demo pairs at full size against oracle hashes
+    (tests/golden/make_config_hashes.py): the Middlebury Motorcycle pair of config C
+    (1482x994, D=[0,256]); 0600 (1280x720) in ROI mode (maxD := W/2 = 640, 641 labels) and in
+    mask mode with the reference's default HSI model."""
+    import hashlib
+    import json
+
+    gold = json.load(open(os.path.join(GOLDEN, "config_hashes.json"))).get(case)
+    if gold is None:
+        pytest.fail(f"no committed oracle hash for {case}")
+    if case == "MOTO":
+        d = os.path.join(GOLDEN, "demo")
+        left, right = load_bgr(os.path.join(d, "Motorcycle_Left.png")), load_bgr(os.path.join(d, "Motorcycle_Right.png"))
+    else:
+        left, right = demo_pair_0600
+    model = gold.get("color_model", 0)
+    d_g, _ = _gpu(matcher, tsm, left, right, model, 0, gold["max_disparity"],
+                  roi=bool(gold.get("roi_matching", 0)), mask=bool(gold.get("mask_matching", 0)))
+    matcher.setMatchingStrategy(tsm.ColorModel.RGB)
+    d_g = np.ascontiguousarray(d_g, dtype=np.float32)
+    assert list(d_g.shape) == gold["shape"]
+    assert abs(float((d_g >= 0).mean()) - gold["valid_fraction"]) < 1e-12
+    assert hashlib.sha256(d_g.tobytes()).hexdigest() == gold["sha256"]
