@@ -38,6 +38,13 @@ int tsm_apply_colormap_device(const float* d_disp, int rows, int cols, size_t st
                               const uint8_t* lut768, int use_range, float min_val, float max_val,
                               uint8_t* d_bgr, size_t out_step, void* hip_stream);
 
+/* Group form: n maps of one size (n <= any; launched 64 maps at a time), e.g. a batch's
+ * outputs straight from tsm_adc_compute_batch_device.  Per map, the same result as the
+ * single call (auto range: each map's own min / max). */
+int tsm_apply_colormap_batch_device(int n, const float* const* d_disps, int rows, int cols, size_t step,
+                                    const uint8_t* lut768, int use_range, float min_val, float max_val,
+                                    uint8_t* const* d_bgrs, size_t out_step, void* hip_stream);
+
 /* ---- f3: reprojection and point clouds (source/stereo.cpp:136-356) --------- */
 
 /* stereo::reprojectToDepth (stereo.cpp:136-148): depth = f*b / d, 0 where d < 0 or inf. */
@@ -46,6 +53,11 @@ int tsm_reproject_to_depth(const float* disp, int rows, int cols, size_t step, f
 int tsm_reproject_to_depth_device(const float* d_disp, int rows, int cols, size_t step, float focal,
                                   float baseline, float* d_depth, size_t out_step, void* hip_stream);
 
+/* Group form (n maps of one size, 64 a launch). */
+int tsm_reproject_to_depth_batch_device(int n, const float* const* d_disps, int rows, int cols, size_t step,
+                                        float focal, float baseline, float* const* d_depths, size_t out_step,
+                                        void* hip_stream);
+
 /* stereo::reprojectTo3D(disparity, f, b, cx, cy, XYZ) (stereo.cpp:150-169): xyz is
  * rows x cols x 3 fp32 (CV_32FC3), 0 where d < 0 or inf. */
 int tsm_reproject_to_3d(const float* disp, int rows, int cols, size_t step, float focal,
@@ -53,6 +65,11 @@ int tsm_reproject_to_3d(const float* disp, int rows, int cols, size_t step, floa
 int tsm_reproject_to_3d_device(const float* d_disp, int rows, int cols, size_t step, float focal,
                                float baseline, float cx, float cy, float* d_xyz, size_t out_step,
                                void* hip_stream);
+
+/* Group form (n maps of one size, 64 a launch). */
+int tsm_reproject_to_3d_batch_device(int n, const float* const* d_disps, int rows, int cols, size_t step,
+                                     float focal, float baseline, float cx, float cy, float* const* d_xyzs,
+                                     size_t out_step, void* hip_stream);
 
 /* stereo::reprojectTo3D(disparity, Q, XYZ) (stereo.cpp:171-202): [x y z w] = Q [u v d 1]
  * with Q (row-major 4x4, CV_64F) converted to fp32, then x/w, y/w, z/w. */
@@ -83,6 +100,12 @@ int tsm_remap_linear_fixed_device(const uint8_t* d_src, int src_rows, int src_co
                                   int channels, const int16_t* d_xy, size_t xy_step,
                                   const uint16_t* d_fxy, size_t fxy_step, int rows, int cols,
                                   uint8_t* d_dst, size_t dst_step, void* hip_stream);
+/* Group form: n images of one size through the same maps (every left view of a batch
+ * through the left maps, EpipolarRectify.cpp:99), 64 a launch. */
+int tsm_remap_linear_fixed_batch_device(int n, const uint8_t* const* d_srcs, int src_rows, int src_cols,
+                                        size_t src_step, int channels, const int16_t* d_xy, size_t xy_step,
+                                        const uint16_t* d_fxy, size_t fxy_step, int rows, int cols,
+                                        uint8_t* const* d_dsts, size_t dst_step, void* hip_stream);
 /* Same with CV_32FC1 x / y maps (rounded to 1/32 pixel, as cv::remap converts them). */
 int tsm_remap_linear_float(const uint8_t* src, int src_rows, int src_cols, size_t src_step,
                            int channels, const float* mapx, const float* mapy, size_t map_step,

@@ -9,7 +9,8 @@ from .adcensus import ADCensus, ADCensusError, CensusWin, ColorModel  # noqa: F4
 from ._native import LIB_PATH, device_count, version  # noqa: F401
 from . import synthetic  # noqa: F401
 from .stereo_ops import (EpipolarRectify, EpipolarRectifyMap, JETColorMap, applyColorMap,  # noqa: F401
-                         remap, reprojectTo3D, reprojectToDepth, writePointCloudToPCD,
+                         applyColorMapBatch, remap, remapBatch, reprojectTo3D, reprojectTo3DBatch,
+                         reprojectToDepth, reprojectToDepthBatch, writePointCloudToPCD,
                          writePointCloudToPLY)
 
 __all__ = ["ADCensus", "ADCensusError", "CensusWin", "ColorModel", "LIB_PATH", "device_count",

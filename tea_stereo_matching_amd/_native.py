@@ -109,6 +109,11 @@ OPS_SIGNATURES = {
     "tsm_remap_linear_fixed_device": (_i, [_P, _i, _i, _z, _i, _P, _z, _P, _z, _i, _i, _P, _z, _P]),
     "tsm_remap_linear_float": (_i, [_P, _i, _i, _z, _i, _P, _P, _z, _i, _i, _P, _z]),
     "tsm_remap_linear_float_device": (_i, [_P, _i, _i, _z, _i, _P, _P, _z, _i, _i, _P, _z, _P]),
+    # group forms: n maps through one launch (pointer arrays of device buffers)
+    "tsm_apply_colormap_batch_device": (_i, [_i, _P, _i, _i, _z, _P, _i, _f, _f, _P, _z, _P]),
+    "tsm_reproject_to_depth_batch_device": (_i, [_i, _P, _i, _i, _z, _f, _f, _P, _z, _P]),
+    "tsm_reproject_to_3d_batch_device": (_i, [_i, _P, _i, _i, _z, _f, _f, _f, _f, _P, _z, _P]),
+    "tsm_remap_linear_fixed_batch_device": (_i, [_i, _P, _i, _i, _z, _i, _P, _z, _P, _z, _i, _i, _P, _z, _P]),
 }
 
 _lib = None

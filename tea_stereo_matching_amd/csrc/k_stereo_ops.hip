@@ -5,7 +5,10 @@
 //   f4  cv::remap INTER_LINEAR of EpipolarRectify::rectify (EpipolarRectify.cpp:87-101)
 // All are HBM-bound streams: 4 pixels a lane along a row, so the byte-wide BGR outputs
 // leave as whole dwords (12 B a lane), and no divergent per-pixel branches beyond the
-// reference's own validity tests.
+// reference's own validity tests.  Every kernel takes tables of up to kOpsBatch maps
+// (blockIdx.z = map): the _batch_device forms run a whole group of the matcher's outputs
+// in one launch (one map per call is launch-latency bound at config-B sizes); the single
+// forms are a table of one.
 #include <hip/hip_runtime.h>
 #include <math.h>
 #include <stdint.h>
@@ -22,6 +25,12 @@ namespace {
 
 constexpr int OPS_THREADS = 256;
 constexpr int OPS_PX = 4;  // pixels per lane along a row
+constexpr int kOpsBatch = 64;  // maps per launch (pointer tables ride in the kernel arguments)
+
+template <class T>
+struct Tab {
+    T* p[kOpsBatch];
+};
 
 // (unsigned char)t with x86 cvttss2si semantics: NaN / out of int range -> 0x80000000
 __device__ __forceinline__ uint32_t cast_u8_x86(float t) {
@@ -71,10 +80,12 @@ __device__ __forceinline__ void block_minmax(uint32_t& lo, int& hi, uint32_t* s_
     }
 }
 
-__global__ void k_minmax(const float* __restrict__ src, int rows, int cols, size_t step_f,
-                         uint32_t* __restrict__ part) {
+// part: MM_BLOCKS partial pairs per map (map z at part + 2 * MM_BLOCKS * z)
+__global__ void k_minmax(Tab<const float> srcs, int rows, int cols, size_t step_f, uint32_t* __restrict__ part) {
     __shared__ uint32_t s_lo[16];
     __shared__ int s_hi[16];
+    const float* __restrict__ src = srcs.p[blockIdx.z];
+    part += (size_t)2 * MM_BLOCKS * blockIdx.z;
     const int n = rows * cols;
     uint32_t lo = 0x7f800000u;
     int hi = (int)0xff800000u;  // -inf: no valid pixel
@@ -94,9 +105,12 @@ __global__ void k_minmax(const float* __restrict__ src, int rows, int cols, size
     }
 }
 
+// mm: the folded (min, max) of map z at mm + 2 z
 __global__ void k_minmax_final(uint32_t* __restrict__ part, int nparts, uint32_t* __restrict__ mm) {
     __shared__ uint32_t s_lo[16];
     __shared__ int s_hi[16];
+    part += (size_t)2 * MM_BLOCKS * blockIdx.z;
+    mm += 2 * blockIdx.z;
     uint32_t lo = 0x7f800000u;
     int hi = (int)0xff800000u;
     for (int i = threadIdx.x; i < nparts; i += blockDim.x) {
@@ -110,11 +124,14 @@ __global__ void k_minmax_final(uint32_t* __restrict__ part, int nparts, uint32_t
     }
 }
 
-__global__ void k_colormap(const float* __restrict__ src, int rows, int cols, size_t step_f,
+__global__ void k_colormap(Tab<const float> srcs, int rows, int cols, size_t step_f,
                            const uint32_t* __restrict__ mm, int use_range, float rmin, float rmax,
-                           Lut lut, uint8_t* __restrict__ dst, size_t dstep) {
+                           Lut lut, Tab<uint8_t> dsts, size_t dstep) {
     const RowGrid p = row_grid(cols);
     if (p.x0 >= cols) return;
+    const float* __restrict__ src = srcs.p[blockIdx.z];
+    uint8_t* __restrict__ dst = dsts.p[blockIdx.z];
+    if (!use_range) mm += 2 * blockIdx.z;
     const float mn = use_range ? rmin : __uint_as_float(mm[0]);
     const float mx = use_range ? rmax : __int_as_float((int)mm[1]);
     const float* s = src + (size_t)p.y * step_f;
@@ -143,10 +160,12 @@ __global__ void k_colormap(const float* __restrict__ src, int rows, int cols, si
 
 // ---- f3 ---------------------------------------------------------------------------
 
-__global__ void k_depth(const float* __restrict__ src, int rows, int cols, size_t step_f, float fb,
-                        float* __restrict__ dst, size_t dstep_f) {
+__global__ void k_depth(Tab<const float> srcs, int rows, int cols, size_t step_f, float fb,
+                        Tab<float> dsts, size_t dstep_f) {
     const RowGrid p = row_grid(cols);
     if (p.x0 >= cols) return;
+    const float* __restrict__ src = srcs.p[blockIdx.z];
+    float* __restrict__ dst = dsts.p[blockIdx.z];
     const int n = min(OPS_PX, cols - p.x0);
     for (int k = 0; k < n; ++k) {
         const float d = src[(size_t)p.y * step_f + p.x0 + k];
@@ -158,10 +177,12 @@ struct F3 {
     float x, y, z;
 };
 
-__global__ void k_xyz(const float* __restrict__ src, int rows, int cols, size_t step_f, float f,
-                      float fb, float cx, float cy, float* __restrict__ dst, size_t dstep_f) {
+__global__ void k_xyz(Tab<const float> srcs, int rows, int cols, size_t step_f, float f,
+                      float fb, float cx, float cy, Tab<float> dsts, size_t dstep_f) {
     const RowGrid p = row_grid(cols);
     if (p.x0 >= cols) return;
+    const float* __restrict__ src = srcs.p[blockIdx.z];
+    float* __restrict__ dst = dsts.p[blockIdx.z];
     const int n = min(OPS_PX, cols - p.x0);
     const float v = (float)p.y;
     for (int k = 0; k < n; ++k) {
@@ -181,10 +202,12 @@ struct Q16 {
     float q[16];
 };
 
-__global__ void k_xyz_q(const float* __restrict__ src, int rows, int cols, size_t step_f, Q16 Q,
-                        float* __restrict__ dst, size_t dstep_f) {
+__global__ void k_xyz_q(Tab<const float> srcs, int rows, int cols, size_t step_f, Q16 Q,
+                        Tab<float> dsts, size_t dstep_f) {
     const RowGrid p = row_grid(cols);
     if (p.x0 >= cols) return;
+    const float* __restrict__ src = srcs.p[blockIdx.z];
+    float* __restrict__ dst = dsts.p[blockIdx.z];
     const int n = min(OPS_PX, cols - p.x0);
     for (int k = 0; k < n; ++k) {
         const int u = p.x0 + k;
@@ -269,12 +292,14 @@ __device__ __forceinline__ void store_px(uint8_t* d, int n, const uint32_t (&o)[
 }
 
 template <int C>
-__global__ void k_remap_fixed(const uint8_t* __restrict__ src, int sh, int sw, size_t sstep,
+__global__ void k_remap_fixed(Tab<const uint8_t> srcs, int sh, int sw, size_t sstep,
                               const int16_t* __restrict__ xy, size_t xy_step_e,
                               const uint16_t* __restrict__ fxy, size_t fxy_step_e, int rows, int cols,
-                              uint8_t* __restrict__ dst, size_t dstep) {
+                              Tab<uint8_t> dsts, size_t dstep) {
     const RowGrid p = row_grid(cols);
     if (p.x0 >= cols) return;
+    const uint8_t* __restrict__ src = srcs.p[blockIdx.z];
+    uint8_t* __restrict__ dst = dsts.p[blockIdx.z];
     const int n = min(OPS_PX, cols - p.x0);
     uint32_t o[OPS_PX][C];
 #pragma unroll
@@ -295,12 +320,14 @@ __device__ __forceinline__ int round32(float v) {
 }
 
 template <int C>
-__global__ void k_remap_float(const uint8_t* __restrict__ src, int sh, int sw, size_t sstep,
+__global__ void k_remap_float(Tab<const uint8_t> srcs, int sh, int sw, size_t sstep,
                               const float* __restrict__ mapx, const float* __restrict__ mapy,
-                              size_t map_step_f, int rows, int cols, uint8_t* __restrict__ dst,
+                              size_t map_step_f, int rows, int cols, Tab<uint8_t> dsts,
                               size_t dstep) {
     const RowGrid p = row_grid(cols);
     if (p.x0 >= cols) return;
+    const uint8_t* __restrict__ src = srcs.p[blockIdx.z];
+    uint8_t* __restrict__ dst = dsts.p[blockIdx.z];
     const int n = min(OPS_PX, cols - p.x0);
     uint32_t o[OPS_PX][C];
 #pragma unroll
@@ -316,9 +343,28 @@ __global__ void k_remap_float(const uint8_t* __restrict__ src, int sh, int sw, s
 
 // ---- host side --------------------------------------------------------------------
 
-dim3 row_blocks(int rows, int cols) {
+dim3 row_blocks(int rows, int cols, int n = 1) {
     const int groups = (cols + OPS_PX - 1) / OPS_PX;
-    return dim3((groups + OPS_THREADS - 1) / OPS_THREADS, rows);
+    return dim3((groups + OPS_THREADS - 1) / OPS_THREADS, rows, n);
+}
+
+template <class T, class U>
+Tab<T> tab_of(const U* const* ptrs, int n) {
+    Tab<T> t{};
+    for (int i = 0; i < n; ++i) t.p[i] = const_cast<T*>(reinterpret_cast<const T*>(ptrs[i]));
+    return t;
+}
+template <class T, class U>
+Tab<T> tab_one(U* p) {
+    Tab<T> t{};
+    t.p[0] = const_cast<T*>(reinterpret_cast<const T*>(p));
+    return t;
+}
+bool null_in(const void* const* ptrs, int n) {
+    if (!ptrs) return true;
+    for (int i = 0; i < n; ++i)
+        if (!ptrs[i]) return true;
+    return false;
 }
 
 bool bad_dims(int rows, int cols) { return rows <= 0 || cols <= 0; }
@@ -371,7 +417,8 @@ int host_form(const void* in, size_t in_row, size_t in_step, int rows, void* out
 }
 
 
-constexpr size_t MM_SCRATCH_BYTES = (size_t)(2 * MM_BLOCKS + 2) * 4;
+// [0, 2 kOpsBatch): folded (min, max) per map; then MM_BLOCKS partial pairs per map
+constexpr size_t MM_SCRATCH_BYTES = (size_t)(2 * kOpsBatch + 2 * MM_BLOCKS * kOpsBatch) * 4;
 
 // the min/max scratch of the _device form: one buffer per (device, stream), kept for the
 // process lifetime (launches on one stream are ordered, so reuse is safe)
@@ -386,19 +433,23 @@ uint32_t* stream_scratch(void* stream) {
     return (uint32_t*)p;
 }
 
-int colormap_launch(const float* d_disp, int rows, int cols, size_t step, const uint8_t* lut768, int use_range,
-                    float min_val, float max_val, uint8_t* d_bgr, size_t out_step, uint32_t* scratch,
-                    hipStream_t st) {
+// nm maps (<= kOpsBatch) of one size; the min/max scratch holds every map's folds
+int colormap_launch(const Tab<const float>& src, int nm, int rows, int cols, size_t step, const uint8_t* lut768,
+                    int use_range, float min_val, float max_val, const Tab<uint8_t>& dst, size_t out_step,
+                    uint32_t* scratch, hipStream_t st) {
     const Lut L = make_lut(lut768);
-    uint32_t* mm = scratch;  // [0..1] folded min / max, then MM_BLOCKS partial pairs
+    uint32_t* mm = scratch;
     if (!use_range) {
         const int n = rows * cols;
-        const int blocks = min((n + OPS_THREADS - 1) / OPS_THREADS, MM_BLOCKS);
-        hipLaunchKernelGGL(k_minmax, dim3(blocks), dim3(OPS_THREADS), 0, st, d_disp, rows, cols, step / 4, mm + 2);
-        hipLaunchKernelGGL(k_minmax_final, dim3(1), dim3(1024), 0, st, mm + 2, blocks, mm);
+        // fewer partial blocks per map when the launch carries many maps (the chip is full)
+        const int per_map = max(8, MM_BLOCKS / nm);
+        const int blocks = min((n + OPS_THREADS - 1) / OPS_THREADS, per_map);
+        hipLaunchKernelGGL(k_minmax, dim3(blocks, 1, nm), dim3(OPS_THREADS), 0, st, src, rows, cols, step / 4,
+                           mm + 2 * kOpsBatch);
+        hipLaunchKernelGGL(k_minmax_final, dim3(1, 1, nm), dim3(1024), 0, st, mm + 2 * kOpsBatch, blocks, mm);
     }
-    hipLaunchKernelGGL(k_colormap, row_blocks(rows, cols), dim3(OPS_THREADS), 0, st, d_disp, rows, cols,
-                       step / 4, mm, use_range, min_val, max_val, L, d_bgr, out_step);
+    hipLaunchKernelGGL(k_colormap, row_blocks(rows, cols, nm), dim3(OPS_THREADS), 0, st, src, rows, cols,
+                       step / 4, mm, use_range, min_val, max_val, L, dst, out_step);
     return status(hipGetLastError());
 }
 
@@ -442,8 +493,29 @@ int tsm_apply_colormap_device(const float* d_disp, int rows, int cols, size_t st
         scratch = stream_scratch(hip_stream);
         if (!scratch) return TSM_ERR_OUT_OF_MEMORY;
     }
-    return colormap_launch(d_disp, rows, cols, step, lut768, use_range, min_val, max_val, d_bgr, out_step,
-                           scratch, (hipStream_t)hip_stream);
+    return colormap_launch(tab_one<const float>(d_disp), 1, rows, cols, step, lut768, use_range, min_val, max_val,
+                           tab_one<uint8_t>(d_bgr), out_step, scratch, (hipStream_t)hip_stream);
+}
+
+int tsm_apply_colormap_batch_device(int n, const float* const* d_disps, int rows, int cols, size_t step,
+                                    const uint8_t* lut768, int use_range, float min_val, float max_val,
+                                    uint8_t* const* d_bgrs, size_t out_step, void* hip_stream) {
+    if (n < 0 || (n > 0 && (null_in((const void* const*)d_disps, n) || null_in((const void* const*)d_bgrs, n))) ||
+        bad_dims(rows, cols) || step % 4 || step < 4 * (size_t)cols || out_step < 3 * (size_t)cols)
+        return TSM_ERR_ARGUMENT;
+    uint32_t* scratch = nullptr;
+    if (!use_range && n > 0) {
+        scratch = stream_scratch(hip_stream);
+        if (!scratch) return TSM_ERR_OUT_OF_MEMORY;
+    }
+    for (int i = 0; i < n; i += kOpsBatch) {  // the scratch is reused chunk after chunk (stream order)
+        const int k = min(kOpsBatch, n - i);
+        const int rc = colormap_launch(tab_of<const float>(d_disps + i, k), k, rows, cols, step, lut768, use_range,
+                                       min_val, max_val, tab_of<uint8_t>(d_bgrs + i, k), out_step, scratch,
+                                       (hipStream_t)hip_stream);
+        if (rc != TSM_OK) return rc;
+    }
+    return TSM_OK;
 }
 
 int tsm_apply_colormap(const float* disp, int rows, int cols, size_t step, const uint8_t* lut768,
@@ -455,8 +527,9 @@ int tsm_apply_colormap(const float* disp, int rows, int cols, size_t step, const
     if (scratch.e != hipSuccess) return status(scratch.e);
     return host_form(disp, 4 * (size_t)cols, step, rows, bgr, 3 * (size_t)cols, out_step,
                      [&](void* di, size_t is, void* dout, size_t os) {
-                         int rc = colormap_launch((const float*)di, rows, cols, is, lut768, use_range, min_val,
-                                                  max_val, (uint8_t*)dout, os, (uint32_t*)scratch.p, nullptr);
+                         int rc = colormap_launch(tab_one<const float>(di), 1, rows, cols, is, lut768, use_range,
+                                                  min_val, max_val, tab_one<uint8_t>(dout), os,
+                                                  (uint32_t*)scratch.p, nullptr);
                          return rc != TSM_OK ? rc : status(hipDeviceSynchronize());
                      });
 }
@@ -467,7 +540,23 @@ int tsm_reproject_to_depth_device(const float* d_disp, int rows, int cols, size_
         step < 4 * (size_t)cols || out_step < 4 * (size_t)cols)
         return TSM_ERR_ARGUMENT;
     hipLaunchKernelGGL(k_depth, row_blocks(rows, cols), dim3(OPS_THREADS), 0, (hipStream_t)hip_stream,
-                       d_disp, rows, cols, step / 4, focal * baseline, d_depth, out_step / 4);
+                       tab_one<const float>(d_disp), rows, cols, step / 4, focal * baseline,
+                       tab_one<float>(d_depth), out_step / 4);
+    return status(hipGetLastError());
+}
+
+int tsm_reproject_to_depth_batch_device(int n, const float* const* d_disps, int rows, int cols, size_t step,
+                                        float focal, float baseline, float* const* d_depths, size_t out_step,
+                                        void* hip_stream) {
+    if (n < 0 || (n > 0 && (null_in((const void* const*)d_disps, n) || null_in((const void* const*)d_depths, n))) ||
+        bad_dims(rows, cols) || step % 4 || out_step % 4 || step < 4 * (size_t)cols || out_step < 4 * (size_t)cols)
+        return TSM_ERR_ARGUMENT;
+    for (int i = 0; i < n; i += kOpsBatch) {
+        const int k = min(kOpsBatch, n - i);
+        hipLaunchKernelGGL(k_depth, row_blocks(rows, cols, k), dim3(OPS_THREADS), 0, (hipStream_t)hip_stream,
+                           tab_of<const float>(d_disps + i, k), rows, cols, step / 4, focal * baseline,
+                           tab_of<float>(d_depths + i, k), out_step / 4);
+    }
     return status(hipGetLastError());
 }
 
@@ -490,7 +579,23 @@ int tsm_reproject_to_3d_device(const float* d_disp, int rows, int cols, size_t s
         step < 4 * (size_t)cols || out_step < 12 * (size_t)cols)
         return TSM_ERR_ARGUMENT;
     hipLaunchKernelGGL(k_xyz, row_blocks(rows, cols), dim3(OPS_THREADS), 0, (hipStream_t)hip_stream,
-                       d_disp, rows, cols, step / 4, focal, focal * baseline, cx, cy, d_xyz, out_step / 4);
+                       tab_one<const float>(d_disp), rows, cols, step / 4, focal, focal * baseline, cx, cy,
+                       tab_one<float>(d_xyz), out_step / 4);
+    return status(hipGetLastError());
+}
+
+int tsm_reproject_to_3d_batch_device(int n, const float* const* d_disps, int rows, int cols, size_t step,
+                                     float focal, float baseline, float cx, float cy, float* const* d_xyzs,
+                                     size_t out_step, void* hip_stream) {
+    if (n < 0 || (n > 0 && (null_in((const void* const*)d_disps, n) || null_in((const void* const*)d_xyzs, n))) ||
+        bad_dims(rows, cols) || step % 4 || out_step % 4 || step < 4 * (size_t)cols || out_step < 12 * (size_t)cols)
+        return TSM_ERR_ARGUMENT;
+    for (int i = 0; i < n; i += kOpsBatch) {
+        const int k = min(kOpsBatch, n - i);
+        hipLaunchKernelGGL(k_xyz, row_blocks(rows, cols, k), dim3(OPS_THREADS), 0, (hipStream_t)hip_stream,
+                           tab_of<const float>(d_disps + i, k), rows, cols, step / 4, focal, focal * baseline, cx,
+                           cy, tab_of<float>(d_xyzs + i, k), out_step / 4);
+    }
     return status(hipGetLastError());
 }
 
@@ -514,7 +619,7 @@ int tsm_reproject_to_3d_q_device(const float* d_disp, int rows, int cols, size_t
     Q16 Q;
     for (int i = 0; i < 16; ++i) Q.q[i] = (float)q16[i];  // Q.convertTo(CV_32F), stereo.cpp:190
     hipLaunchKernelGGL(k_xyz_q, row_blocks(rows, cols), dim3(OPS_THREADS), 0, (hipStream_t)hip_stream,
-                       d_disp, rows, cols, step / 4, Q, d_xyz, out_step / 4);
+                       tab_one<const float>(d_disp), rows, cols, step / 4, Q, tab_one<float>(d_xyz), out_step / 4);
     return status(hipGetLastError());
 }
 
@@ -539,15 +644,34 @@ int tsm_remap_linear_fixed_device(const uint8_t* d_src, int src_rows, int src_co
         (C != 1 && C != 3 && C != 4) || src_step < (size_t)C * src_cols || xy_step % 2 || fxy_step % 2 ||
         xy_step < 4 * (size_t)cols || fxy_step < 2 * (size_t)cols || dst_step < (size_t)C * cols)
         return TSM_ERR_ARGUMENT;
+    return tsm_remap_linear_fixed_batch_device(1, &d_src, src_rows, src_cols, src_step, C, d_xy, xy_step, d_fxy,
+                                               fxy_step, rows, cols, &d_dst, dst_step, hip_stream);
+}
+
+int tsm_remap_linear_fixed_batch_device(int n, const uint8_t* const* d_srcs, int src_rows, int src_cols,
+                                        size_t src_step, int channels, const int16_t* d_xy, size_t xy_step,
+                                        const uint16_t* d_fxy, size_t fxy_step, int rows, int cols,
+                                        uint8_t* const* d_dsts, size_t dst_step, void* hip_stream) {
+    const int C = channels;
+    if (n < 0 || (n > 0 && (null_in((const void* const*)d_srcs, n) || null_in((const void* const*)d_dsts, n))) ||
+        !d_xy || !d_fxy || bad_dims(rows, cols) || bad_dims(src_rows, src_cols) ||
+        (C != 1 && C != 3 && C != 4) || src_step < (size_t)C * src_cols || xy_step % 2 || fxy_step % 2 ||
+        xy_step < 4 * (size_t)cols || fxy_step < 2 * (size_t)cols || dst_step < (size_t)C * cols)
+        return TSM_ERR_ARGUMENT;
     hipStream_t st = (hipStream_t)hip_stream;
-    const dim3 g = row_blocks(rows, cols);
-#define TSM_REMAP_FIXED(CC)                                                                       \
-    hipLaunchKernelGGL(k_remap_fixed<CC>, g, dim3(OPS_THREADS), 0, st, d_src, src_rows, src_cols, \
-                       src_step, d_xy, xy_step / 2, d_fxy, fxy_step / 2, rows, cols, d_dst, dst_step)
-    if (C == 1) TSM_REMAP_FIXED(1);
-    else if (C == 3) TSM_REMAP_FIXED(3);
-    else TSM_REMAP_FIXED(4);
+    for (int i = 0; i < n; i += kOpsBatch) {
+        const int k = min(kOpsBatch, n - i);
+        const dim3 g = row_blocks(rows, cols, k);
+        const Tab<const uint8_t> s = tab_of<const uint8_t>(d_srcs + i, k);
+        const Tab<uint8_t> d = tab_of<uint8_t>(d_dsts + i, k);
+#define TSM_REMAP_FIXED(CC)                                                                               \
+        hipLaunchKernelGGL(k_remap_fixed<CC>, g, dim3(OPS_THREADS), 0, st, s, src_rows, src_cols, src_step, \
+                           d_xy, xy_step / 2, d_fxy, fxy_step / 2, rows, cols, d, dst_step)
+        if (C == 1) TSM_REMAP_FIXED(1);
+        else if (C == 3) TSM_REMAP_FIXED(3);
+        else TSM_REMAP_FIXED(4);
 #undef TSM_REMAP_FIXED
+    }
     return status(hipGetLastError());
 }
 
@@ -562,9 +686,11 @@ int tsm_remap_linear_float_device(const uint8_t* d_src, int src_rows, int src_co
         return TSM_ERR_ARGUMENT;
     hipStream_t st = (hipStream_t)hip_stream;
     const dim3 g = row_blocks(rows, cols);
-#define TSM_REMAP_FLOAT(CC)                                                                       \
-    hipLaunchKernelGGL(k_remap_float<CC>, g, dim3(OPS_THREADS), 0, st, d_src, src_rows, src_cols, \
-                       src_step, d_mapx, d_mapy, map_step / 4, rows, cols, d_dst, dst_step)
+    const Tab<const uint8_t> s = tab_one<const uint8_t>(d_src);
+    const Tab<uint8_t> d = tab_one<uint8_t>(d_dst);
+#define TSM_REMAP_FLOAT(CC)                                                                               \
+    hipLaunchKernelGGL(k_remap_float<CC>, g, dim3(OPS_THREADS), 0, st, s, src_rows, src_cols, src_step, \
+                       d_mapx, d_mapy, map_step / 4, rows, cols, d, dst_step)
     if (C == 1) TSM_REMAP_FLOAT(1);
     else if (C == 3) TSM_REMAP_FLOAT(3);
     else TSM_REMAP_FLOAT(4);

@@ -201,6 +201,80 @@ def remap(src, map1, map2):
     return dst
 
 
+# ---- group forms (device tensors): a batch's maps through one launch per 64 ----------
+
+def _ptr_array(ts):
+    return (ctypes.c_void_p * len(ts))(*[t.data_ptr() for t in ts])
+
+
+def _dev_batch(srcs, what):
+    srcs = [t.contiguous() for t in srcs]
+    if not srcs or not all(_is_dev(t) for t in srcs) or len({tuple(t.shape) for t in srcs}) != 1:
+        raise ValueError(f"{what}: expected a non-empty list of device tensors of one shape")
+    return srcs
+
+
+def applyColorMapBatch(disparities, colorMap=None, minVal=None, maxVal=None):
+    """applyColorMap over a list of (H, W) float32 device tensors (tsm_apply_colormap_batch_device):
+    per map the same image as applyColorMap; returns a list of (H, W, 3) uint8 tensors."""
+    import torch
+
+    ss = _dev_batch([_f32(d) for d in disparities], "applyColorMapBatch")
+    H, W = ss[0].shape
+    lut = np.ascontiguousarray(np.asarray(JETColorMap() if colorMap is None else colorMap,
+                                          dtype=np.uint8).reshape(256, 3))
+    use_range = minVal is not None
+    outs = [torch.empty((H, W, 3), dtype=torch.uint8, device=ss[0].device) for _ in ss]
+    rc = N.load().tsm_apply_colormap_batch_device(len(ss), _ptr_array(ss), H, W, 4 * W, _ptr(lut), int(use_range),
+                                                  float(minVal or 0.0), float(maxVal or 0.0), _ptr_array(outs),
+                                                  3 * W, _stream())
+    _check(_done(rc, True), "applyColorMapBatch")
+    return outs
+
+
+def reprojectToDepthBatch(disparities, focalLength: float, baseline: float):
+    """reprojectToDepth over a list of device tensors (tsm_reproject_to_depth_batch_device)."""
+    import torch
+
+    ss = _dev_batch([_f32(d) for d in disparities], "reprojectToDepthBatch")
+    H, W = ss[0].shape
+    outs = [torch.empty((H, W), dtype=torch.float32, device=ss[0].device) for _ in ss]
+    rc = N.load().tsm_reproject_to_depth_batch_device(len(ss), _ptr_array(ss), H, W, 4 * W, focalLength, baseline,
+                                                      _ptr_array(outs), 4 * W, _stream())
+    _check(_done(rc, True), "reprojectToDepthBatch")
+    return outs
+
+
+def reprojectTo3DBatch(disparities, focalLength: float, baseline: float, cx: float, cy: float):
+    """reprojectTo3D(d, f, b, cx, cy) over a list of device tensors (tsm_reproject_to_3d_batch_device)."""
+    import torch
+
+    ss = _dev_batch([_f32(d) for d in disparities], "reprojectTo3DBatch")
+    H, W = ss[0].shape
+    outs = [torch.empty((H, W, 3), dtype=torch.float32, device=ss[0].device) for _ in ss]
+    rc = N.load().tsm_reproject_to_3d_batch_device(len(ss), _ptr_array(ss), H, W, 4 * W, focalLength, baseline, cx,
+                                                   cy, _ptr_array(outs), 12 * W, _stream())
+    _check(_done(rc, True), "reprojectTo3DBatch")
+    return outs
+
+
+def remapBatch(srcs, map1, map2):
+    """cv::remap INTER_LINEAR of a list of device images of one size through the same
+    CV_16SC2 + CV_16UC1 maps (tsm_remap_linear_fixed_batch_device)."""
+    import torch
+
+    ss = _dev_batch(srcs, "remapBatch")
+    C = 1 if ss[0].dim() == 2 else ss[0].shape[2]
+    sh, sw = ss[0].shape[:2]
+    m1, m2 = map1.contiguous(), map2.contiguous()
+    H, W = m2.shape
+    outs = [torch.empty((H, W, C) if C > 1 else (H, W), dtype=torch.uint8, device=ss[0].device) for _ in ss]
+    rc = N.load().tsm_remap_linear_fixed_batch_device(len(ss), _ptr_array(ss), sh, sw, C * sw, C, _ptr(m1), 4 * W,
+                                                      _ptr(m2), 2 * W, H, W, _ptr_array(outs), C * W, _stream())
+    _check(_done(rc, True), "remapBatch")
+    return outs
+
+
 @dataclass
 class EpipolarRectifyMap:
     """stereo::EpipolarRectifyMap (stereo_utils.h / stereo_utils.cpp:88-174): rectification

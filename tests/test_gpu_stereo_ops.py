@@ -205,3 +205,47 @@ def test_epipolar_rectify_side_by_side(tsm, oracle):
     exp_l, exp_r = oracle.remap_linear_fixed(left, xy0, f0), oracle.remap_linear_fixed(right, xy1, f1)
     assert np.array_equal(l2, exp_l) and np.array_equal(r2, exp_r)
     assert np.array_equal(both, np.concatenate([exp_l, exp_r], 1))
+
+
+def test_group_forms_equal_single_calls(tsm, oracle):
+    """The group forms (one launch per 64 maps) give every map the single call's result:
+    70 maps of odd size (a full launch of 64 + 6), each map its own auto colour range."""
+    import torch
+
+    rng = np.random.default_rng(77)
+    H, W = 37, 61
+    ds = [_disp(rng, H, W) for _ in range(70)]
+    ds[5][:] = -1.0  # no valid pixel
+    dev = [torch.from_numpy(d).cuda() for d in ds]
+    lut = tsm.JETColorMap()
+    cols = tsm.applyColorMapBatch(dev, lut)
+    for d, c in zip(ds, cols):
+        assert np.array_equal(c.cpu().numpy(), oracle.apply_colormap_ex(d))
+    cols = tsm.applyColorMapBatch(dev, lut, 10.0, 150.0)
+    for d, c in zip(ds, cols):
+        assert np.array_equal(c.cpu().numpy(), oracle.apply_colormap_ex(d, min_val=10.0, max_val=150.0))
+    for d, o in zip(ds, tsm.reprojectToDepthBatch(dev, 721.5, 0.54)):
+        assert np.array_equal(o.cpu().numpy(), oracle.reproject_to_depth(d, 721.5, 0.54))
+    for d, o in zip(ds, tsm.reprojectTo3DBatch(dev, 721.5, 0.54, 30.2, 17.9)):
+        assert np.array_equal(o.cpu().numpy(), oracle.reproject_to_3d(d, 721.5, 0.54, 30.2, 17.9))
+    imgs = [rng.integers(0, 256, (40, 66, 3), dtype=np.uint8) for _ in range(67)]
+    yy, xx = np.mgrid[0:H, 0:W]
+    ix = (xx * 32 + rng.integers(-40, 40, (H, W))).astype(np.int64)
+    iy = (yy * 32 + rng.integers(-40, 40, (H, W))).astype(np.int64)
+    xy = np.stack([ix >> 5, iy >> 5], -1).astype(np.int16)
+    fxy = ((iy & 31) * 32 + (ix & 31)).astype(np.uint16)
+    outs = tsm.remapBatch([torch.from_numpy(i).cuda() for i in imgs], torch.from_numpy(xy).cuda(),
+                          torch.from_numpy(fxy.view(np.int16)).cuda())
+    for i, o in zip(imgs, outs):
+        assert np.array_equal(o.cpu().numpy(), oracle.remap_linear_fixed(i, xy, fxy))
+
+
+def test_group_forms_reject_bad_tables(tsm):
+    from tea_stereo_matching_amd import _native as N
+
+    lib = N.load()
+    P = ctypes.c_void_p
+    two_null = (P * 2)(None, None)
+    assert lib.tsm_apply_colormap_batch_device(2, two_null, 4, 4, 16, None, 0, 0.0, 0.0, two_null, 12, None) == N.TSM_ERR_ARGUMENT
+    assert lib.tsm_reproject_to_depth_batch_device(-1, None, 4, 4, 16, 1.0, 1.0, None, 16, None) == N.TSM_ERR_ARGUMENT
+    assert lib.tsm_reproject_to_depth_batch_device(0, None, 4, 4, 16, 1.0, 1.0, None, 16, None) == N.TSM_OK
