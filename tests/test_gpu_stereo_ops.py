@@ -225,9 +225,9 @@ def test_group_forms_equal_single_calls(tsm, oracle):
     for d, c in zip(ds, cols):
         assert np.array_equal(c.cpu().numpy(), oracle.apply_colormap_ex(d, min_val=10.0, max_val=150.0))
     for d, o in zip(ds, tsm.reprojectToDepthBatch(dev, 721.5, 0.54)):
-        assert np.array_equal(o.cpu().numpy(), oracle.reproject_to_depth(d, 721.5, 0.54))
+        assert np.array_equal(o.cpu().numpy(), oracle.reproject_to_depth(d, 721.5, 0.54), equal_nan=True)
     for d, o in zip(ds, tsm.reprojectTo3DBatch(dev, 721.5, 0.54, 30.2, 17.9)):
-        assert np.array_equal(o.cpu().numpy(), oracle.reproject_to_3d(d, 721.5, 0.54, 30.2, 17.9))
+        assert np.array_equal(o.cpu().numpy(), oracle.reproject_to_3d(d, 721.5, 0.54, 30.2, 17.9), equal_nan=True)
     imgs = [rng.integers(0, 256, (40, 66, 3), dtype=np.uint8) for _ in range(67)]
     yy, xx = np.mgrid[0:H, 0:W]
     ix = (xx * 32 + rng.integers(-40, 40, (H, W))).astype(np.int64)
