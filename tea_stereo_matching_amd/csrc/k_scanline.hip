@@ -22,6 +22,8 @@
 //    is prefetched SC_K steps ahead into a register ring.
 // Optional emulation of the reference's racy omp-static schedule for T threads: the
 // first pixel of each of the T chunks reads its predecessor's pre-pass vector.
+#include <utility>
+
 #include "tsm_device.h"
 #include "tsm_launch.h"
 
@@ -55,6 +57,9 @@ __device__ __forceinline__ uint32_t umin3(uint32_t a, uint32_t b, uint32_t c) {
 // wave min of non-negative floats held as bits (+inf padding is neutral).  VG: keep it in
 // VGPRs via the gfx950 lane swaps (faster on the scanline's serial chain when every
 // consumer is a vector op; the WTA's scalar uses prefer the readlane form).
+template <int N>
+struct IC { static constexpr int value = N; };
+
 template <int J, bool VG = false>
 __device__ __forceinline__ uint32_t vec_min_bits(const f32x4 (&x)[J]) {
     uint32_t m = min(min(fbits(x[0][0]), fbits(x[0][1])), min(fbits(x[0][2]), fbits(x[0][3])));
@@ -193,7 +198,9 @@ __device__ __forceinline__ void scan_issue(StepIn<J>& s, int pos, int dir, int l
 #pragma unroll
     for (int j = 0; j < J; ++j) s.p[j] = *reinterpret_cast<const f32x4*>(pv[j]);  // (nt loads: -2 %)
     const uint32_t i1 = (uint32_t)(HORIZ ? C.gpad + pm : pm * C.gstride + C.gpad + line);
-    s.d1 = (int)__builtin_amdgcn_raw_buffer_load_b8(R.own, 0u, orow + i1, 0);
+    // d1 as the aligned dword holding its byte (a byte load's value is narrowed by the
+    // compiler, which then re-widens every ring slot at the loop back-edge, waiting for it)
+    s.d1 = (int)__builtin_amdgcn_raw_buffer_load_b32(R.own, 0u, (orow + i1) & ~3u, 0);
     s.mk = 1u;
     if (MASK) {
         const uint32_t ii = (uint32_t)(HORIZ ? line * C.W + (pos - dir) : (pos - dir) * C.W + line);
@@ -365,71 +372,99 @@ __global__ __launch_bounds__(256) void k_scan_line(float* __restrict__ vol,
 #pragma unroll
             for (int j = 0; j < J; ++j) pf[j] += dstep[j];
         }
+        // slots issued in order (the loop's waits assume slot k is the k-th oldest load set)
+        __builtin_amdgcn_sched_barrier(0);
     }
     int pfi = SC_K < n ? SC_K : n - 1;  // step index pf points at (clamped to the last)
 
     static_assert(64 % SC_K == 0, "WTA groups of 64 steps hold whole unrolled blocks");
     int dacc = 0;  // WTA: indices of the current group of 64 steps, one per lane
-    for (int b = 0; b < n; b += SC_K) {
+    // one step: ring slot k (compile-time), step index it
+    auto step = [&](auto Kc, int it) {
+        constexpr int k = decltype(Kc)::value;
+        const StepIn<J>& s = ring[k];
+        const int pos = posbase + dir * it;
+        const uint32_t sh = (uint32_t)((HORIZ ? x0a + pos : x0a) & 3);
+        if (OMP) {
+            if (it == cs) {  // chunk start of the racy schedule: stale predecessor
 #pragma unroll
-        for (int k = 0; k < SC_K; ++k) {
-            const int it = b + k;
-            if (it < n) {
-                const StepIn<J>& s = ring[k];
-                const int pos = posbase + dir * it;
-                const uint32_t sh = (uint32_t)((HORIZ ? x0a + pos : x0a) & 3);
-                if (OMP) {
-                    if (it == cs) {  // chunk start of the racy schedule: stale predecessor
+                for (int j = 0; j < J; ++j) q[j] = qorig[j];
+                mq = mqorig;
+                ++ct;
+                cs = ct < T ? omp_start(ct, n, T) : 0x7fffffff;
+            }
+            if (it + 1 == cs) {  // the next chunk's first pixel sees this pre-pass vector
 #pragma unroll
-                        for (int j = 0; j < J; ++j) q[j] = qorig[j];
-                        mq = mqorig;
-                        ++ct;
-                        cs = ct < T ? omp_start(ct, n, T) : 0x7fffffff;
-                    }
-                    if (it + 1 == cs) {  // the next chunk's first pixel sees this pre-pass vector
-#pragma unroll
-                        for (int j = 0; j < J; ++j) qorig[j] = s.p[j];
-                        mqorig = vec_min_bits<J>(s.p);
-                    }
-                }
-                const bool masked = MASK && __builtin_amdgcn_readfirstlane(s.mk) == 0;  // :824, :862
-                // :880-881: m == 0 leaves p untouched (branch-free: compute, then select)
-                f32x4 np[J];
-#pragma unroll
-                for (int j = 0; j < J; ++j) np[j] = s.p[j];
-                const int d1 = __builtin_amdgcn_readfirstlane(s.d1);
-                partial_opt<J>(np, q, mq, d1, s, psel0 + sh * 0x01010101u, lane, C);
-                const bool upd = !(masked || mq == 0u);
-#pragma unroll
-                for (int j = 0; j < J; ++j) q[j] = upd ? np[j] : s.p[j];
-                if (store && upd) {  // untouched vectors are not rewritten
-#pragma unroll
-                    for (int j = 0; j < J; ++j)
-                        st_stream(cur[j], q[j]);
-                }
-#pragma unroll
-                for (int j = 0; j < J; ++j) cur[j] += dstep[j];
-                mq = vec_min_bits<J, true>(q);
-                if (WTA) {  // step it's index lands in lane it & 63, stored 64 steps at a time
-                    const int d = vec_argmin_nb<J>(q, lane, C.L, C.minD, mq);  // whole wave
-                    dacc = lane == (it & 63) ? d : dacc;
-                }
-                // refill this slot only now that its data is consumed (a load into a live
-                // slot would make the compiler stage it in temporaries and copy it back,
-                // waiting for the load right away)
-                scan_issue<J, HORIZ, MASK>(ring[k], posbase + dir * pfi, dir, line, pf, gv, R, orow, sgn, C);
-                if (pfi + 1 < n) {
-                    ++pfi;
-#pragma unroll
-                    for (int j = 0; j < J; ++j) pf[j] += dstep[j];
-                }
+                for (int j = 0; j < J; ++j) qorig[j] = s.p[j];
+                mqorig = vec_min_bits<J>(s.p);
             }
         }
-        if (WTA && (((b + SC_K) & 63) == 0 || b + SC_K >= n)) {  // flush a group of 64 steps
-            const int g0 = b & ~63;
-            if (lane < min(n, g0 + 64) - g0) wrow[posbase + dir * (g0 + lane)] = dacc;
+        const bool masked = MASK && __builtin_amdgcn_readfirstlane(s.mk) == 0;  // :824, :862
+        // :880-881: m == 0 leaves p untouched (branch-free: compute, then select)
+        f32x4 np[J];
+#pragma unroll
+        for (int j = 0; j < J; ++j) np[j] = s.p[j];
+        const uint32_t i1 = (uint32_t)(HORIZ ? C.gpad + (dir > 0 ? pos : pos + 1)
+                                             : (dir > 0 ? pos : pos + 1) * C.gstride + C.gpad + line);
+        const int d1 = ((uint32_t)__builtin_amdgcn_readfirstlane(s.d1) >> (8 * ((orow + i1) & 3u))) & 0xff;
+        partial_opt<J>(np, q, mq, d1, s, psel0 + sh * 0x01010101u, lane, C);
+        const bool upd = !(masked || mq == 0u);
+        // q gets registers of its own (early-clobber copy): coalesced with the ring slot, it
+        // would keep the slot's registers live past the refill, and the compiler would then
+        // rotate the whole ring by copies at the loop back-edge (each copy waiting for its
+        // in-flight load: the prefetch gone)
+#pragma unroll
+        for (int j = 0; j < J; ++j) {
+            const f32x4 sel = upd ? np[j] : s.p[j];
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+                float o;
+                asm volatile("v_mov_b32 %0, %1" : "=&v"(o) : "v"(sel[e]));
+                q[j][e] = o;
+            }
         }
+        if (store && upd) {  // untouched vectors are not rewritten
+#pragma unroll
+            for (int j = 0; j < J; ++j) st_stream(cur[j], q[j]);
+        }
+#pragma unroll
+        for (int j = 0; j < J; ++j) cur[j] += dstep[j];
+        mq = vec_min_bits<J, true>(q);
+        if (WTA) {  // step it's index lands in lane it & 63, stored 64 steps at a time
+            const int d = vec_argmin_nb<J>(q, lane, C.L, C.minD, mq);  // whole wave
+            dacc = lane == (it & 63) ? d : dacc;
+        }
+        // refill this slot only now that its data is consumed (a load into a live slot would
+        // make the compiler stage it in temporaries and copy it back, waiting for the load
+        // right away); past the line end the last pixel is re-read (a select, no branch)
+        scan_issue<J, HORIZ, MASK>(ring[k], posbase + dir * pfi, dir, line, pf, gv, R, orow, sgn, C);
+        const bool adv = pfi + 1 < n;
+        pfi = adv ? pfi + 1 : pfi;
+#pragma unroll
+        for (int j = 0; j < J; ++j) pf[j] += adv ? dstep[j] : 0;
+        // keep the refill in its step: the scheduler otherwise sinks early slots' loads to the
+        // block end, and the next block's first steps wait for them almost at once
+        __builtin_amdgcn_sched_barrier(0);
+    };
+    auto flush_wta = [&](int b) {  // the group of 64 steps holding step b
+        const int g0 = b & ~63;
+        if (lane < min(n, g0 + 64) - g0) wrow[posbase + dir * (g0 + lane)] = dacc;
+    };
+    // Whole blocks of SC_K steps as straight-line code (no per-step range branches): the
+    // waitcnt pass then counts each slot's loads across the loop back-edge, so a step waits
+    // only for its own prefetched data (with range branches it drained vmcnt(0) at every
+    // block, one full memory latency per SC_K steps).
+    int b = 0;
+    for (; b + SC_K <= n; b += SC_K) {
+        [&]<int... Ks>(std::integer_sequence<int, Ks...>) {
+            (step(IC<Ks>{}, b + Ks), ...);
+        }(std::make_integer_sequence<int, SC_K>{});
+        if (WTA && ((b + SC_K) & 63) == 0) flush_wta(b);
     }
+    [&]<int... Ks>(std::integer_sequence<int, Ks...>) {
+        ((b + Ks < n ? step(IC<Ks>{}, b + Ks) : (void)0), ...);
+    }(std::make_integer_sequence<int, SC_K>{});
+    if (WTA && (n & 63) != 0) flush_wta(n - 1);
 }
 
 template <int J, int K, bool HORIZ, bool MASK, bool WTA>
@@ -461,8 +496,13 @@ static int launch_scan(float* vol, const uint8_t* grad, const uint32_t* img, int
     // a horizontal pass of one or two pairs runs under one wave per SIMD: the deeper ring
     const bool deep = HORIZ && P.npairs <= 2;
     if (J == 1) {
-        if (deep) launch_scan_m<1, 16, HORIZ, WTA>(vol, grad, img, dir, wta, store_view1, infvec, P, st);
-        else launch_scan_m<1, 8, HORIZ, WTA>(vol, grad, img, dir, wta, store_view1, infvec, P, st);
+        if constexpr (HORIZ) {
+            if (deep) launch_scan_m<1, 16, HORIZ, WTA>(vol, grad, img, dir, wta, store_view1, infvec, P, st);
+            else launch_scan_m<1, 8, HORIZ, WTA>(vol, grad, img, dir, wta, store_view1, infvec, P, st);
+        } else {
+            (void)deep;
+            launch_scan_m<1, 8, HORIZ, WTA>(vol, grad, img, dir, wta, store_view1, infvec, P, st);
+        }
     } else if (J == 2) {
         launch_scan_m<2, 8, HORIZ, WTA>(vol, grad, img, dir, wta, store_view1, infvec, P, st);
     } else if (J == 3) {
