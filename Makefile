@@ -16,7 +16,14 @@ CPP_SRCS := engine stereo_api stereo_ops stereo_ops_api
 OBJS     := $(addprefix $(OBJ)/,$(addsuffix .o,$(HIP_SRCS) $(CPP_SRCS)))
 HDRS     := $(SRC)/tsm_device.h $(SRC)/tsm_launch.h include/tsm_adcensus.h include/stereo.h include/tsm_stereo_ops.h
 
-all: lib oracle
+all: lib oracle probe
+
+# HBM calibration kernels for bench.py (measurement tooling, not the product)
+PROBE    := tools/lib/libtsm_hbm_probe.so
+probe: $(PROBE)
+$(PROBE): tools/micro/hbm_probe.hip
+	@mkdir -p tools/lib
+	$(HIPCC) --offload-arch=$(ARCH) -O3 -std=c++20 -fPIC -Wno-unused-result -shared -o $@ $<
 
 lib: $(LIB)
 
@@ -46,4 +53,4 @@ clean:
 	rm -rf build $(LIBDIR)
 	$(MAKE) -C oracle clean
 
-.PHONY: all lib oracle clean exp
+.PHONY: all lib oracle clean exp probe

@@ -498,190 +498,6 @@ __global__ __launch_bounds__(CW_THREADS) __attribute__((amdgpu_waves_per_eu(E ==
 }
 
 // ---------------------------------------------------------------------------
-// cost-volume build by square tiles of the (left pixel, right pixel) band: every cell
-// computed once for BOTH views (minD = 0, no mask)
-// ---------------------------------------------------------------------------
-// With minD = 0 the two views hold the same cells: view 0 pairs left(x0) with right(x0 - k)
-// and view 1 pairs right(x1) with left(x1 + k), so C1(x1, k) = C0(x1 + k, k) -- census,
-// AD and the border rule (:562-566: either window off the image) are all symmetric in
-// (left, right).  A cell is the pair (x0, x1), k = x0 - x1 in [0, L).  A wave owns a
-// 64 x 64 tile of that band: lane i holds the right record of x1 = b + i in registers for
-// the whole tile, and the 64 steps r walk the left pixels x0 = a + r (a = b + 64 m,
-// k = 64 m + r - i), whose records are staged in LDS and read as broadcasts.  No lane
-// shifts: a step is the census (6 x and, and_or, bcnt), one v_sad_u8 and two table reads.
-//   view 0: step r's 64 cells are labels 64 m + r - 63 .. 64 m + r of pixel x0: one
-//     256-B store (lane i writes label 64 m + r - i);
-//   view 1: lane i's cells over the steps are consecutive labels of pixel x1 = b + i:
-//     kept 16 steps in a per-wave LDS buffer, then stored 64 B a pixel (4 pixels an
-//     instruction).
-// A workgroup holds the M + 1 tiles of one right-pixel block b (m = 0..M), so a view-1
-// vector's pieces leave together; consecutive blocks of a row run on one XCD, so a view-0
-// vector's pieces (blocks b = a - 64 m) meet in its L2.  Against the walk (two views, a
-// lane-shift register): about 40 % fewer vector instructions per cell for 25 % of cells
-// computed outside the band (the tile corners).
-constexpr int CT_TILE = 64;
-constexpr int CT_FLUSH = 16;              // view-1 steps buffered per flush
-constexpr int CT_PAD = CT_FLUSH + 1;      // buffer row stride (odd: conflict-free column writes)
-
-__host__ __device__ inline int cost_tile_m(int Lp) { return (Lp - 1 + CT_TILE - 1) / CT_TILE; }  // M
-
-template <bool HSI>
-__global__ __launch_bounds__(1024) void k_cost_tile(const uint32_t* __restrict__ desc, const float* __restrict__ lutA,
-                                                    int lutA_n, const float* __restrict__ lutB,
-                                                    float* __restrict__ vol, DevParams Pk, int nbb) {
-    const DevParams P = Pk;
-    __shared__ __attribute__((aligned(16))) float s_lut[CW_LUTB + (HSI ? 2816 : 768)];
-    extern __shared__ __attribute__((aligned(16))) u32x4 smem_tile[];
-    float* sB = s_lut;
-    float* sA = s_lut + CW_LUTB;
-    const int H = P.H, W = P.W, L = P.L, Lp = P.Lp;
-    const int m = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const int lane = threadIdx.x & 63;
-    pair_shift(blockIdx.z, P.pstride, desc, vol);
-    // XCD-aware block order (as the walk): each XCD takes a contiguous run of (row, b) blocks
-    const int nb = gridDim.x, per = nb >> 3;
-    const int blk = (int)blockIdx.x < 8 * per ? ((int)blockIdx.x & 7) * per + ((int)blockIdx.x >> 3) : (int)blockIdx.x;
-    const int y = blk / nbb;
-    if (y >= H) return;  // whole workgroup (no barrier pending)
-    const int b = (blk - y * nbb - cost_tile_m(Lp)) * CT_TILE;  // first block: x1 >= 1 - Lp
-    const int a = b + CT_TILE * m;
-    const int hw = P.censusW >> 1, hh = P.censusH >> 1;
-    const bool rowok = y - hh >= 0 && y + hh < H;
-    constexpr int NW = HSI ? 11 : 13;
-    constexpr int CWORD = 12;
-    const uint32_t vmask_hi = (P.censusW * P.censusH - 1) >= 64
-                                  ? 0xffffffffu
-                                  : ((1u << ((P.censusW * P.censusH - 1) - 32)) - 1u);
-    const uint32_t* dL = desc + (size_t)y * W * 16;              // left records (view 0 image)
-    const uint32_t* dR = desc + ((size_t)H + y) * W * 16;        // right records
-    float* vol0 = vol + (size_t)y * W * Lp;                      // view 0, row y
-    float* vol1 = vol + ((size_t)H + y) * W * Lp;                // view 1, row y
-    auto clampx = [&](int x) { return x < 0 ? 0 : (x >= W ? W - 1 : x); };
-    // per wave: 64 staged left records (4 KB), then the view-1 transpose buffer
-    u32x4* stF = smem_tile + (size_t)m * (CT_TILE * 4 + (CT_TILE * CT_PAD + 3) / 4);
-    float* tb = reinterpret_cast<float*>(stF + CT_TILE * 4);
-
-    // k range of this tile: 64 m + r - i, r, i in [0, 64)
-    const int klo_t = CT_TILE * m - (CT_TILE - 1), khi_t = CT_TILE * m + (CT_TILE - 1);
-    const bool any_x0 = a + CT_TILE > 0 && a < W;      // view-0 outputs
-    const bool any_x1 = b + CT_TILE > 0 && b < W;      // view-1 outputs
-    const bool live = (any_x0 || any_x1) && khi_t >= 0 && klo_t < Lp;
-    // cells needing the census: some k < L with both pixels' windows inside the image
-    const bool compute = live && rowok && klo_t < L && a + CT_TILE > hw && a < W - hw && b + CT_TILE > hw &&
-                         b < W - hw;
-    if (compute) {  // stage the tile's left records (LDS-DMA: lane j's 16 B land at base + 16 j)
-#pragma unroll
-        for (int c = 0; c < 4; ++c) {
-            const int t = 16 * c + (lane >> 2);
-            __builtin_amdgcn_global_load_lds(reinterpret_cast<const u32x4*>(dL + (size_t)clampx(a + t) * 16) + (lane & 3),
-                                             stF + 64 * c, 16, 0, 0);
-        }
-    }
-    for (int i = threadIdx.x; i < lutA_n; i += blockDim.x) sA[i] = 2.f - lutA[i];
-    for (int i = threadIdx.x; i < CW_LUTB; i += blockDim.x) sB[i] = i < 188 ? lutB[i] : 0.f;
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-    if (!live) return;
-
-    const int x1 = b + lane;
-    const bool x1ok = x1 >= hw && x1 < W - hw;  // this lane's right window inside the image
-    uint32_t V[NW];
-    {
-        const u32x4* r = reinterpret_cast<const u32x4*>(dR + (size_t)clampx(x1) * 16);
-        const u32x4 q0 = r[0], q1 = r[1], q2 = r[2], q3 = r[3];
-        const uint32_t rec[13] = {q0.x, q0.y, q0.z, q0.w, q1.x, q1.y, q1.z, q1.w, q2.x, q2.y, q2.z, q2.w, q3.x};
-#pragma unroll
-        for (int w = 0; w < NW; ++w) V[w] = rec[w < NW - 1 ? w : CWORD];
-    }
-    const float kInf = __int_as_float(0x7f800000);
-    // view-1 addresses: lane i of a flush instruction t4 serves pixel p = 4 t4 + (i >> 4),
-    // label slot s = i & 15 of the block of 16 steps
-    const int fp = lane >> 4, fs = lane & 15;
-
-    auto cell = [&](const uint32_t (&F)[NW]) -> float {
-        uint32_t cen = 0;
-        if (!HSI) {
-#pragma unroll
-            for (int w = 0; w < 6; ++w) cen = bcnt_acc((F[w] & V[6 + w]) | (F[6 + w] & V[w]), cen);
-        } else {
-            cen = __builtin_popcount(~(F[0] & V[0])) + __builtin_popcount(~(F[1] & V[1]) & vmask_hi);
-#pragma unroll
-            for (int w = 2; w < 6; ++w) cen += __builtin_popcount((F[w] & V[4 + w]) | (F[4 + w] & V[w]));
-        }
-        const uint32_t fc = F[NW - 1], vc = V[NW - 1];
-        int ai;
-        if (!HSI) {
-            ai = (int)__builtin_amdgcn_sad_u8(fc, vc, 0u);
-        } else {
-            const int hd = (int)__builtin_amdgcn_sad_u8(fc & 0xffu, vc & 0xffu, 0u);
-            ai = 2 * min(hd, 255 - hd) + 5 * (int)__builtin_amdgcn_sad_u8(fc & 0xffff00u, vc & 0xffff00u, 0u);
-        }
-        return sA[ai] - sB[cen];
-    };
-    auto load_F = [&](int t, uint32_t (&F)[NW]) {
-        const u32x4* s = stF + 4 * t;
-        const u32x4 q0 = s[0], q1 = s[1], q2 = s[2];
-        const uint32_t c = reinterpret_cast<const uint32_t*>(s)[CWORD];
-        const uint32_t rec[13] = {q0.x, q0.y, q0.z, q0.w, q1.x, q1.y, q1.z, q1.w, q2.x, q2.y, q2.z, q2.w, c};
-#pragma unroll
-        for (int w = 0; w < NW; ++w) F[w] = rec[w < NW - 1 ? w : CWORD];
-    };
-    // the whole tile inside the image and the label band (no selects, every store lands)
-    const bool fast = compute && a >= hw && a + CT_TILE <= W - hw && b >= hw && b + CT_TILE <= W - hw &&
-                      klo_t >= 0 && khi_t < L;
-    // store addresses: a wave-uniform row pointer (SGPRs) + a lane-constant offset, so a
-    // store is global_store_dword off the scalar base with no per-step vector arithmetic
-    //   view 0 step r: vol0 + x0 Lp + 64 m + r - 63, lane offset 63 - i (label 64 m + r - i)
-    //   view 1 flush: pixel b + 4 t4 + fp, label 64 m + r0 - 4 t4 + fs - fp
-    const int o0 = CT_TILE - 1 - lane;
-    const int o1 = fp * (Lp - 1) + fs;
-    auto run = [&](auto FASTc) {
-        constexpr bool FAST = decltype(FASTc)::value;
-        for (int r0 = 0; r0 < CT_TILE; r0 += CT_FLUSH) {
-#pragma unroll 4
-            for (int s = 0; s < CT_FLUSH; ++s) {
-                const int r = r0 + s;
-                const int x0 = a + r;
-                float c;
-                if constexpr (FAST) {
-                    uint32_t F[NW];
-                    load_F(r, F);
-                    c = cell(F);
-                } else {
-                    const int k = CT_TILE * m + r - lane;
-                    float cc = 2.f;
-                    if (compute && x0 >= hw && x0 < W - hw) {
-                        uint32_t F[NW];
-                        load_F(r, F);
-                        cc = cell(F);
-                        cc = x1ok ? cc : 2.f;
-                    }
-                    c = k >= L ? kInf : cc;
-                }
-                float* p0 = vol0 + (ptrdiff_t)x0 * Lp + (CT_TILE * m + r - (CT_TILE - 1));
-                if (FAST || (x0 >= 0 && x0 < W && (unsigned)(CT_TILE * m + r - lane) < (unsigned)Lp)) p0[o0] = c;
-                tb[lane * CT_PAD + s] = c;  // view 1: pixel x1 = b + lane, label 64 m + r - lane
-            }
-            // flush: pixel p's 16 labels 64 m + r0 - p .. + 15 (64 B), four pixels an instruction
-#pragma unroll 4
-            for (int t4 = 0; t4 < CT_TILE / 4; ++t4) {
-                const int p = 4 * t4 + fp;
-                const float v = tb[p * CT_PAD + fs];
-                float* p1 = vol1 + (ptrdiff_t)(b + 4 * t4) * Lp + (CT_TILE * m + r0 - 4 * t4);
-                if (FAST || (b + p >= 0 && b + p < W && (unsigned)(CT_TILE * m + r0 + fs - p) < (unsigned)Lp)) p1[o1] = v;
-            }
-        }
-    };
-    if (fast) run(IC<true>{});
-    else run(IC<false>{});
-}
-
-size_t cost_tile_lds_bytes(const DevParams& P) {
-    const int waves = cost_tile_m(P.Lp) + 1;
-    return (size_t)waves * (CT_TILE * 4 + (CT_TILE * CT_PAD + 3) / 4) * 16;
-}
-
-// ---------------------------------------------------------------------------
 // launchers
 // ---------------------------------------------------------------------------
 void launch_pack(const PairIn& in, size_t step, uint32_t* img, const DevParams& P, hipStream_t st) {
@@ -752,34 +568,9 @@ static void launch_cost_t(const uint32_t* desc, const float* lutA, int lutA_n, c
     trace_point("k_cost_walk", st);
 }
 
-template <bool HSI>
-static void launch_cost_tile_t(const uint32_t* desc, const float* lutA, int lutA_n, const float* lutB, float* vol,
-                               const DevParams& P, hipStream_t st) {
-    static bool attr = false;
-    if (!attr) {
-        (void)hipFuncSetAttribute((const void*)k_cost_tile<HSI>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                  160 * 1024 - 4 * (CW_LUTB + (HSI ? 2816 : 768)));
-        attr = true;
-    }
-    const int M = cost_tile_m(P.Lp);
-    const int nbb = M + (P.W + CT_TILE - 1) / CT_TILE;  // right-pixel blocks from 1 - Lp to W - 1
-    hipLaunchKernelGGL((k_cost_tile<HSI>), dim3(P.H * nbb, 1, P.npairs), dim3(64 * (M + 1)), cost_tile_lds_bytes(P),
-                       st, desc, lutA, lutA_n, lutB, vol, P, nbb);
-    trace_point("k_cost_tile", st);
-}
-
-// The tile build serves minD = 0 outside mask mode (the views share their cells) up to
-// 16 waves a tile column (Lp <= 961); the walk serves every other range and mode.
-static bool cost_use_tile(const DevParams& P) { return P.minD == 0 && !P.mask && cost_tile_m(P.Lp) + 1 <= 16; }
-
 int launch_cost_volume(const uint32_t* desc, const float* lutA, int lutA_n, const float* lutB, float* vol,
                        const DevParams& P, hipStream_t st) {
     const bool hsi = P.color_model == 1;
-    if (cost_use_tile(P)) {
-        if (hsi) launch_cost_tile_t<true>(desc, lutA, lutA_n, lutB, vol, P, st);
-        else launch_cost_tile_t<false>(desc, lutA, lutA_n, lutB, vol, P, st);
-        return 0;
-    }
 #define CASE(E)                                                                                  \
     if (hsi) {                                                                                     \
         if (P.mask) launch_cost_t<E, true, true>(desc, lutA, lutA_n, lutB, vol, P, st);            \

@@ -443,8 +443,9 @@ __global__ __launch_bounds__(256) void k_scan_line(float* __restrict__ vol,
 #pragma unroll
         for (int j = 0; j < J; ++j) pf[j] += adv ? dstep[j] : 0;
         // keep the refill in its step: the scheduler otherwise sinks early slots' loads to the
-        // block end, and the next block's first steps wait for them almost at once
-        __builtin_amdgcn_sched_barrier(0);
+        // block end, and the next block's first steps wait for them almost at once (ALU work
+        // may still cross: mask 0x7 = ALU / VALU / SALU)
+        __builtin_amdgcn_sched_barrier(0x7);
     };
     auto flush_wta = [&](int b) {  // the group of 64 steps holding step b
         const int g0 = b & ~63;
