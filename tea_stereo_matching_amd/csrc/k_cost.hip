@@ -96,35 +96,46 @@ __global__ void k_gauss_median(const uint32_t* __restrict__ src, uint32_t* __res
 // load.  Border pixels (window leaving the image) never reach the cost (:562-566):
 // their planes are zero.
 // ---------------------------------------------------------------------------
+constexpr int CD_TX = 128;  // pixels of a row per workgroup
+
 template <int CW, int CHh, bool HSI>
-__global__ void k_census_desc(const uint32_t* __restrict__ img, uint32_t* __restrict__ desc,
-                              DevParams Pk) {
+__global__ __launch_bounds__(CD_TX) void k_census_desc(const uint32_t* __restrict__ img, uint32_t* __restrict__ desc,
+                                                       DevParams Pk) {
     const DevParams P = Pk;  // kernel args -> registers once (no per-use kernarg reloads)
-    const int x = blockIdx.x * blockDim.x + threadIdx.x;
+    constexpr int hw = CW / 2, hh = CHh / 2;
+    constexpr int TW = CD_TX + 2 * hw;  // the window's rows for the block's pixels, staged in LDS
+    __shared__ uint32_t s_win[CHh][TW];
+    const int x0 = blockIdx.x * CD_TX;
+    const int x = x0 + threadIdx.x;
     const int y = blockIdx.y;
     const int v = blockIdx.z & 1;
     const int H = P.H, W = P.W;
-    if (x >= W) return;
     pair_shift(blockIdx.z >> 1, P.pstride, img, desc);
-    constexpr int hw = CW / 2, hh = CHh / 2;
+    const uint32_t* im = img + (size_t)v * H * W;
+    for (int i = threadIdx.x; i < CHh * TW; i += CD_TX) {
+        const int r = i / TW, c = i - r * TW;
+        const int yy = y - hh + r, xx = x0 - hw + c;
+        s_win[r][c] = (yy >= 0 && yy < H && xx >= 0 && xx < W) ? im[(size_t)yy * W + xx] : 0u;
+    }
+    __syncthreads();
+    if (x >= W) return;
     uint32_t w[12];
 #pragma unroll
     for (int k = 0; k < 12; ++k) w[k] = 0;
-    const uint32_t* im = img + (size_t)v * H * W;
-    const uint32_t c = im[(size_t)y * W + x];
+    const int tx = threadIdx.x + hw;
+    const uint32_t c = s_win[hh][tx];
     if (x - hw >= 0 && x + hw < W && y - hh >= 0 && y + hh < H) {
         const int c0 = ch(c, 0), c1 = ch(c, 1), c2 = ch(c, 2);
         // fully unrolled: bit position and word index are compile-time constants
 #pragma unroll
         for (int i = -hh; i <= hh; ++i) {
-            const uint32_t* row = im + (size_t)(y + i) * W + x;
 #pragma unroll
             for (int j = -hw; j <= hw; ++j) {
                 if (i == 0 && j == 0) continue;
                 const int bit = (i + hh) * CW + (j + hw) - (((i + hh) * CW + (j + hw)) > (hh * CW + hw) ? 1 : 0);
                 const int wi = bit >> 5;
                 const uint32_t m = 1u << (bit & 31);
-                const uint32_t n = row[j];
+                const uint32_t n = s_win[i + hh][tx + j];
                 if (!HSI) {
                     const int d0 = ch(n, 0) - c0, d1 = ch(n, 1) - c1, d2 = ch(n, 2) - c2;
                     w[0 + wi] |= d0 > 0 ? m : 0u;
@@ -525,14 +536,14 @@ void launch_hsi_convert(const uint32_t* src, uint32_t* dst, int n, int filter, c
 }
 
 void launch_census(const uint32_t* img, uint32_t* desc, const DevParams& P, hipStream_t st) {
-    dim3 g((P.W + 127) / 128, P.H, 2 * P.npairs);
+    dim3 g((P.W + CD_TX - 1) / CD_TX, P.H, 2 * P.npairs);
     const bool hsi = P.color_model == 1;
     if (P.censusW == 7) {
-        if (hsi) hipLaunchKernelGGL((k_census_desc<7, 5, true>), g, dim3(128), 0, st, img, desc, P);
-        else hipLaunchKernelGGL((k_census_desc<7, 5, false>), g, dim3(128), 0, st, img, desc, P);
+        if (hsi) hipLaunchKernelGGL((k_census_desc<7, 5, true>), g, dim3(CD_TX), 0, st, img, desc, P);
+        else hipLaunchKernelGGL((k_census_desc<7, 5, false>), g, dim3(CD_TX), 0, st, img, desc, P);
     } else {
-        if (hsi) hipLaunchKernelGGL((k_census_desc<9, 7, true>), g, dim3(128), 0, st, img, desc, P);
-        else hipLaunchKernelGGL((k_census_desc<9, 7, false>), g, dim3(128), 0, st, img, desc, P);
+        if (hsi) hipLaunchKernelGGL((k_census_desc<9, 7, true>), g, dim3(CD_TX), 0, st, img, desc, P);
+        else hipLaunchKernelGGL((k_census_desc<9, 7, false>), g, dim3(CD_TX), 0, st, img, desc, P);
     }
     trace_point("k_census_desc", st);
 }

@@ -403,27 +403,39 @@ __device__ __forceinline__ int reflect101(int i, int n) {
 }
 
 // equalizeHist LUT (imgproc histogram.cpp): lut[i] = saturate_cast<uchar>(sum * scale),
-// scale = 255.f / (total - hist[first nonzero]); one wave, serial 256-entry prefix.
-__global__ void k_eq_lut(const int32_t* __restrict__ hist, uint8_t* __restrict__ lut_out, int total, size_t ps) {
+// scale = 255.f / (total - hist[first nonzero]).  One 256-thread block: the running sums
+// are integers (an LDS prefix scan is exact), each entry then one multiply and rint.
+__global__ __launch_bounds__(256) void k_eq_lut(const int32_t* __restrict__ hist, uint8_t* __restrict__ lut_out,
+                                                int total, size_t ps) {
     pair_shift(blockIdx.z, ps, hist, lut_out);
-    if (threadIdx.x != 0) return;
-    uint8_t* lut = lut_out;
-    int i = 0;
-    while (i < 256 && hist[i] == 0) ++i;
-    for (int k = 0; k < 256; ++k) lut[k] = 0;
+    __shared__ int pre[256];
+    __shared__ int first;
+    const int k = threadIdx.x;
+    const int hk = hist[k];
+    pre[k] = hk;
+    if (k == 0) first = 256;
+    __syncthreads();
+    if (hk != 0) atomicMin(&first, k);
+    for (int off = 1; off < 256; off <<= 1) {  // inclusive prefix sums
+        const int add = k >= off ? pre[k - off] : 0;
+        __syncthreads();
+        pre[k] += add;
+        __syncthreads();
+    }
+    const int i = first;
+    uint8_t out = 0;
     if (i < 256) {
-        if (hist[i] == total) {
-            lut[i] = (uint8_t)i;
-        } else {
-            const float scale = (256 - 1.f) / (float)(total - hist[i]);
-            int sum = 0;
-            for (int k = i + 1; k < 256; ++k) {
-                sum += hist[k];
-                const int v = (int)rintf((float)sum * scale);
-                lut[k] = (uint8_t)(v < 0 ? 0 : (v > 255 ? 255 : v));
-            }
+        const int hi = pre[i] - (i > 0 ? pre[i - 1] : 0);
+        if (hi == total) {
+            out = k == i ? (uint8_t)i : 0;
+        } else if (k > i) {
+            const float scale = (256 - 1.f) / (float)(total - hi);
+            const int sum = pre[k] - pre[i];  // hist[i + 1] + ... + hist[k], in the serial order's value
+            const int v = (int)rintf((float)sum * scale);
+            out = (uint8_t)(v < 0 ? 0 : (v > 255 ? 255 : v));
         }
     }
+    lut_out[k] = out;
 }
 
 // blur 3x3 BORDER_REFLECT_101 of the equalised map with the ColumnSum<ushort,uchar>
@@ -801,7 +813,7 @@ void launch_discontinuity(RefineBufs& B, const float* vol0, const DevParams& P,
     hipLaunchKernelGGL(k_zero_u32, grid1d(1, P), dim3(256), 0, st, reinterpret_cast<uint32_t*>(B.hist), 256, ps); trace_point("k_zero_u32", st);
     hipLaunchKernelGGL(k_gray_hist, grid1d(std::min((n + 255) / 256, 1024), P), dim3(256), 0, st, B.dm, B.gray, B.hist, n, ps); trace_point("k_gray_hist", st);
     uint8_t* lut = reinterpret_cast<uint8_t*>(B.hist + 256);
-    hipLaunchKernelGGL(k_eq_lut, grid1d(1, P), dim3(64), 0, st, B.hist, lut, n, ps); trace_point("k_eq_lut", st);
+    hipLaunchKernelGGL(k_eq_lut, grid1d(1, P), dim3(256), 0, st, B.hist, lut, n, ps); trace_point("k_eq_lut", st);
     hipLaunchKernelGGL(k_eq_blur, grid2d(P.W, P.H, 256, P), dim3(256), 0, st, B.gray, lut,
                        B.gray_eq, B.blurred, P.H, P.W, ps); trace_point("k_eq_blur", st);
     hipLaunchKernelGGL(k_sobel, grid2d(P.W, P.H, 256, P), dim3(256), 0, st, B.blurred, B.dx, B.dy, B.mag, P.H, P.W, ps); trace_point("k_sobel", st);
