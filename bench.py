@@ -68,7 +68,19 @@ def cpu_baseline(args, left, right):
     dt = time.perf_counter() - t0
     return {"value": 1.0 / dt, "unit": "pairs/s", "cores": threads, "kind": "port",
             "sample": f"1 synthetic pair (seed 1000) {args.width}x{args.height} D=[0,{args.max_disparity}] "
-                      f"RGB, oracle/ C restatement with OpenMP, {dt:.2f} s/pair"}
+                      f"RGB, oracle/ C restatement with OpenMP, {dt:.2f} s/pair",
+            "host_cpus": os.cpu_count(), "cpu_model": cpu_model()}
+
+
+def cpu_model():
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return None
 
 
 def pmc_traffic():

@@ -53,71 +53,30 @@ __device__ __forceinline__ int compute_limit(const DevParams& P, uint32_t p, int
     return d - 1;
 }
 
-// computeLimits (:661-683) as two LDS-tiled passes, each writing its half of the packed
-// arms word arms[v][y][x] = up | down<<8 | left<<16 | right<<24 (16-bit stores, no race):
-// an arm reads at most maxLength1 pixels along its direction, so a tile plus a halo of
-// maxLength1 pixels holds every pixel its walks can touch, and each step of the walk is
-// an LDS read instead of a dependent L2 round trip.
-constexpr int ARM_TX = 256;  // row pass: pixels per workgroup
-constexpr int ARM_VC = 64;   // column pass: columns per workgroup
-constexpr int ARM_VR = 64;   // column pass: rows per workgroup
-
-// left / right arms: a row segment of ARM_TX pixels with its halo
-__global__ __launch_bounds__(ARM_TX) void k_arms_row(const uint32_t* __restrict__ img, uint32_t* __restrict__ arms,
-                                                     DevParams Pk) {
-    const DevParams P = Pk;
-    extern __shared__ uint32_t s_row[];
-    const int A = P.max_length1 + 1;
-    const int x0 = blockIdx.x * ARM_TX, y = blockIdx.y, v = blockIdx.z & 1;
-    pair_shift(blockIdx.z >> 1, P.pstride, img, arms);
-    const uint32_t* im = img + ((size_t)v * P.H + y) * P.W;
-    for (int i = threadIdx.x; i < ARM_TX + 2 * A; i += ARM_TX) {
-        const int x = x0 - A + i;
-        s_row[i] = (x >= 0 && x < P.W) ? im[x] : 0u;
-    }
-    __syncthreads();
-    const int t = threadIdx.x, x = x0 + t;
+// arms[v][y][x] = up | down<<8 | left<<16 | right<<24  (computeLimits, :661-683): one
+// thread a pixel, its four walks reading the image through L1/L2.  Arms are short on real
+// scenes (mean 2.1 px), so the walks are a few dependent cached loads; staging row and
+// column tiles with a maxLength1 halo in LDS measured slower (round 3: 0.089 -> 0.161 ms a
+// pair for the stage, the column tile serialising 16 pixels a thread).
+__global__ void k_arms(const uint32_t* __restrict__ img, uint32_t* __restrict__ arms, DevParams Pk) {
+    const DevParams P = Pk;  // kernel args -> registers once (no per-use kernarg reloads)
+    const int x = blockIdx.x * blockDim.x + threadIdx.x;
+    const int y = blockIdx.y;
+    const int v = blockIdx.z & 1;
     if (x >= P.W) return;
-    const uint32_t p = s_row[A + t];
-    uint32_t lr = 0;
+    pair_shift(blockIdx.z >> 1, P.pstride, img, arms);
+    const int W = P.W;
+    const uint32_t* row = img + ((size_t)v * P.H + y) * W;
+    const uint32_t p = row[x];
+    uint32_t packed = 0;
     if (!(P.mask && p == 0)) {
-        const uint32_t lf = compute_limit(P, p, x, [&](int k) { return s_row[A + t - k]; });
-        const uint32_t rt = compute_limit(P, p, P.W - 1 - x, [&](int k) { return s_row[A + t + k]; });
-        lr = lf | (rt << 8);
+        const uint32_t up = compute_limit(P, p, y, [&](int k) { return row[x - (ptrdiff_t)k * W]; });
+        const uint32_t dn = compute_limit(P, p, P.H - 1 - y, [&](int k) { return row[x + (ptrdiff_t)k * W]; });
+        const uint32_t lf = compute_limit(P, p, x, [&](int k) { return row[x - k]; });
+        const uint32_t rt = compute_limit(P, p, W - 1 - x, [&](int k) { return row[x + k]; });
+        packed = up | (dn << 8) | (lf << 16) | (rt << 24);
     }
-    reinterpret_cast<uint16_t*>(arms)[2 * (((size_t)v * P.H + y) * P.W + x) + 1] = (uint16_t)lr;
-}
-
-// up / down arms: ARM_VC columns x ARM_VR rows with the halo above and below
-__global__ __launch_bounds__(256) void k_arms_col(const uint32_t* __restrict__ img, uint32_t* __restrict__ arms,
-                                                  DevParams Pk) {
-    const DevParams P = Pk;
-    extern __shared__ uint32_t s_col[];
-    const int A = P.max_length1 + 1;
-    const int x0 = blockIdx.x * ARM_VC, y0 = blockIdx.y * ARM_VR, v = blockIdx.z & 1;
-    pair_shift(blockIdx.z >> 1, P.pstride, img, arms);
-    const uint32_t* im = img + (size_t)v * P.H * P.W;
-    const int rows = ARM_VR + 2 * A;
-    const int c = threadIdx.x & (ARM_VC - 1), r0 = threadIdx.x / ARM_VC;
-    const int x = x0 + c;
-    for (int r = r0; r < rows; r += 256 / ARM_VC) {
-        const int y = y0 - A + r;
-        s_col[r * ARM_VC + c] = (x < P.W && y >= 0 && y < P.H) ? im[(size_t)y * P.W + x] : 0u;
-    }
-    __syncthreads();
-    if (x >= P.W) return;
-    for (int r = r0; r < ARM_VR; r += 256 / ARM_VC) {
-        const int y = y0 + r;
-        if (y >= P.H) break;
-        const uint32_t p = s_col[(A + r) * ARM_VC + c];
-        uint32_t ud = 0;
-        if (!(P.mask && p == 0)) {
-            const uint32_t up = compute_limit(P, p, y, [&](int k) { return s_col[(A + r - k) * ARM_VC + c]; });
-            const uint32_t dn = compute_limit(P, p, P.H - 1 - y, [&](int k) { return s_col[(A + r + k) * ARM_VC + c]; });
-            ud = up | (dn << 8);
-        }
-        reinterpret_cast<uint16_t*>(arms)[2 * (((size_t)v * P.H + y) * P.W + x)] = (uint16_t)ud;
-    }
+    arms[((size_t)v * P.H + y) * W + x] = packed;
 }
 
 __device__ __forceinline__ int arm_up(uint32_t a) { return a & 0xff; }
@@ -945,18 +904,8 @@ int launch_aggregation_pass(float* vol, const uint32_t* arms, const int32_t* ws,
 }
 
 void launch_arms(const uint32_t* img, uint32_t* arms, const DevParams& P, hipStream_t st) {
-    static bool attr = false;
-    if (!attr) {
-        (void)hipFuncSetAttribute((const void*)k_arms_col, hipFuncAttributeMaxDynamicSharedMemorySize, kLdsBytes);
-        attr = true;
-    }
-    const int A = P.max_length1 + 1;  // <= 257: the column tile is at most 64 x 578 x 4 B = 145 KiB
-    hipLaunchKernelGGL(k_arms_row, dim3((P.W + ARM_TX - 1) / ARM_TX, P.H, 2 * P.npairs), dim3(ARM_TX),
-                       (size_t)(ARM_TX + 2 * A) * 4, st, img, arms, P);
-    trace_point("k_arms_row", st);
-    hipLaunchKernelGGL(k_arms_col, dim3((P.W + ARM_VC - 1) / ARM_VC, (P.H + ARM_VR - 1) / ARM_VR, 2 * P.npairs),
-                       dim3(256), (size_t)ARM_VC * (ARM_VR + 2 * A) * 4, st, img, arms, P);
-    trace_point("k_arms_col", st);
+    dim3 g((P.W + 127) / 128, P.H, 2 * P.npairs);
+    hipLaunchKernelGGL(k_arms, g, dim3(128), 0, st, img, arms, P); trace_point("k_arms", st);
 }
 
 void launch_window_sizes(const uint32_t* arms, int32_t* ws, const DevParams& P, hipStream_t st) {

@@ -275,6 +275,9 @@ __global__ __launch_bounds__(CW_THREADS) __attribute__((amdgpu_waves_per_eu(E ==
     const int slots = cost_stage_slots(seg_len, G);
     u32x4* stF = smem_stage + (size_t)wave * 2 * slots * 4;
     u32x4* stE = stF + (size_t)slots * 4;
+    // the unit's tail float4s (Lp = 64 E + 4), one per pixel, computed before the walk
+    f32x4* stT = reinterpret_cast<f32x4*>(smem_stage + (size_t)(CW_THREADS / 64) * 2 * slots * 4) + wave * CW_SEG;
+    const bool tail = (E == 3 || E == 4 || E == 5) && Lp > 64 * E;
     const int rq = lane & 3, rr = lane >> 2;  // this lane's quarter / record of a chunk
     const int eoff = v == 0 ? -kb : kb + vtop;
     auto dma_chunk = [&](int t0) {  // records t0 .. t0+CW_CHUNK-1 (t0 a multiple of CW_CHUNK)
@@ -323,17 +326,71 @@ __global__ __launch_bounds__(CW_THREADS) __attribute__((amdgpu_waves_per_eu(E ==
         pick(st[i + 0], st[i + 1], st[i + 2], u32x4{r1[CWORD], 0u, 0u, 0u}, o);
     };
 
+    // Lp = 64 E + 4 (E = 3: 193..196 labels, 4: 257..260, 5: 321..324): the lanes cover
+    // labels 0 .. 64E-1, the pixel vector's last float4 (labels 64E .. Lp-1, the real ones
+    // < L, the rest +inf padding) is the tail.  Lane l computes pixel x_lo + l's tail here,
+    // before the walk -- its fixed record from the LDS stage, its varying records from L2,
+    // where the warm-up has just brought that row segment -- into LDS; the walk's step for
+    // the pixel stores it beside the pixel's main store, so the two land in one L2 line
+    // while it is still there (a tail stored after the walk reached HBM as separate partial
+    // lines: 46 MB of the launch's 776 MB written, and re-fetched its records: round 3 PMC).
+    if (tail) {
+        if (lane < count) {
+            const int j = x_lo + lane;
+            const float inf = __int_as_float(0x7f800000);
+            uint32_t Fr[NW];
+            load_staged(stF, lane, Fr);
+            const int xf = j + foff;
+            const bool fixed_ok = !rowOut && xf - hw >= 0 && xf + hw < W;
+            const int klo = v == 0 ? j - (W - 1 - hw) : hw - j;
+            const int khi = v == 0 ? j - hw : W - 1 - hw - j;
+            float c4[4];
+#pragma unroll
+            for (int t = 0; t < 4; ++t) {
+                const int k = 64 * E + t;
+                c4[t] = inf;
+                if (k < L) {
+                    uint32_t Vr[NW];
+                    const u32x4* rv = reinterpret_cast<const u32x4*>(dV + (size_t)clampx(v == 0 ? j - k : j + k) * 16);
+                    pick(rv[0], rv[1], rv[2], rv[3], Vr);
+                    uint32_t cen = 0;
+                    if (!HSI) {
+#pragma unroll
+                        for (int w = 0; w < 6; ++w) cen = bcnt_acc((Fr[w] & Vr[6 + w]) | (Fr[6 + w] & Vr[w]), cen);
+                    } else {
+                        cen = __builtin_popcount(~(Fr[0] & Vr[0])) + __builtin_popcount(~(Fr[1] & Vr[1]) & vmask_hi);
+#pragma unroll
+                        for (int w = 2; w < 6; ++w) cen += __builtin_popcount((Fr[w] & Vr[4 + w]) | (Fr[4 + w] & Vr[w]));
+                    }
+                    const uint32_t vc = Vr[NW - 1], fc = Fr[NW - 1];
+                    int ai;
+                    if (!HSI) {
+                        ai = (int)__builtin_amdgcn_sad_u8(fc, vc, 0u);
+                    } else {
+                        const int hd = (int)__builtin_amdgcn_sad_u8(fc & 0xffu, vc & 0xffu, 0u);
+                        ai = 2 * min(hd, 255 - hd) + 5 * (int)__builtin_amdgcn_sad_u8(fc & 0xffff00u, vc & 0xffff00u, 0u);
+                    }
+                    const float c = sA[ai] - sB[cen];
+                    c4[t] = (fixed_ok && k >= klo && k <= khi) ? c : 2.f;
+                }
+            }
+            stT[lane] = f32x4{c4[0], c4[1], c4[2], c4[3]};
+        }
+        __builtin_amdgcn_wave_barrier();  // one wave: its LDS writes precede its reads in order
+    }
+
     // View 0 pairs label k with right(j - k): the next pixel's label k is this pixel's
     // label k-1, so the label axis moves UP one slot per step (slot of offset e at
     // rotation R: (e - R) mod E; DPP wave_shr carries lanes up, lane 0 takes the entering
     // record x = j - kb).  View 1 pairs label k with left(j + k): the label axis moves DOWN
     // (slot (e + R) mod E; wave_shl, lane 63 takes x = j + kb + vtop).
-    auto walk = [&](auto UPc) {
+    auto walk = [&](auto UPc, auto PADc) {
     constexpr bool UP = decltype(UPc)::value == 0;
+    constexpr bool PAD = decltype(PADc)::value != 0;  // some lane label of the slice is >= L
     const float kInf = __int_as_float(0x7f800000);
     uint32_t padoff[E];  // census start: 0, or CW_LUTB for padding labels (+inf cost)
 #pragma unroll
-    for (int e = 0; e < E; ++e) padoff[e] = (!MASK && kb + E * lane + e >= L) ? CW_LUTB : 0u;
+    for (int e = 0; e < E; ++e) padoff[e] = (PAD && !MASK && kb + E * lane + e >= L) ? CW_LUTB : 0u;
     // fixed records double-buffered by step parity (compile-time), no register copies
     uint32_t FA[NW], FB[NW], En[NW];
     load_staged(stF, 0, FA);
@@ -454,57 +511,20 @@ __global__ __launch_bounds__(CW_THREADS) __attribute__((amdgpu_waves_per_eu(E ==
         [&]<int... Ss>(std::integer_sequence<int, Ss...>) {
             (step(IC<Ss>{}, fast, t + Ss), ...);
         }(std::make_integer_sequence<int, G>{});
+        // the group's tail float4s (labels 64E .. 64E+3), lane s for pixel j0 + t + s, a
+        // few steps after those pixels' main stores: both still in L2
+        if (tail && lane < G && t + lane < count)
+            *reinterpret_cast<f32x4*>(vol + (((size_t)v * H + y) * W + j0 + t + lane) * Lp + 64 * E) = stT[t + lane];
     }
     };
-    if (v == 0) walk(IC<0>{});
-    else walk(IC<1>{});
-    // Lp = 64 E + 4 (E = 3: 193..196 labels, 4: 257..260, 5: 321..324): the lanes cover
-    // labels 0 .. 64E-1, the pixel vector's last float4 (labels 64E .. Lp-1, the real ones
-    // < L, the rest +inf padding) is the tail: lane l computes pixel x_lo + l of the unit
-    // from global records (one gather per label, L2-resident)
-    if constexpr (E == 3 || E == 4 || E == 5) {
-        if (Lp > 64 * E && lane < count) {
-            const int j = x_lo + lane;
-            const float inf = __int_as_float(0x7f800000);
-            uint32_t Fr[NW];
-            const u32x4* rf = reinterpret_cast<const u32x4*>(dF + (size_t)clampx(j + foff) * 16);
-            pick(rf[0], rf[1], rf[2], rf[3], Fr);
-            const int xf = j + foff;
-            const bool fixed_ok = !rowOut && xf - hw >= 0 && xf + hw < W;
-            const int klo = v == 0 ? j - (W - 1 - hw) : hw - j;
-            const int khi = v == 0 ? j - hw : W - 1 - hw - j;
-            float c4[4];
-#pragma unroll
-            for (int t = 0; t < 4; ++t) {
-                const int k = 64 * E + t;
-                c4[t] = inf;
-                if (k < L) {
-                    uint32_t Vr[NW];
-                    const u32x4* rv = reinterpret_cast<const u32x4*>(dV + (size_t)clampx(v == 0 ? j - k : j + k) * 16);
-                    pick(rv[0], rv[1], rv[2], rv[3], Vr);
-                    uint32_t cen = 0;
-                    if (!HSI) {
-#pragma unroll
-                        for (int w = 0; w < 6; ++w) cen = bcnt_acc((Fr[w] & Vr[6 + w]) | (Fr[6 + w] & Vr[w]), cen);
-                    } else {
-                        cen = __builtin_popcount(~(Fr[0] & Vr[0])) + __builtin_popcount(~(Fr[1] & Vr[1]) & vmask_hi);
-#pragma unroll
-                        for (int w = 2; w < 6; ++w) cen += __builtin_popcount((Fr[w] & Vr[4 + w]) | (Fr[4 + w] & Vr[w]));
-                    }
-                    const uint32_t vc = Vr[NW - 1], fc = Fr[NW - 1];
-                    int ai;
-                    if (!HSI) {
-                        ai = (int)__builtin_amdgcn_sad_u8(fc, vc, 0u);
-                    } else {
-                        const int hd = (int)__builtin_amdgcn_sad_u8(fc & 0xffu, vc & 0xffu, 0u);
-                        ai = 2 * min(hd, 255 - hd) + 5 * (int)__builtin_amdgcn_sad_u8(fc & 0xffff00u, vc & 0xffff00u, 0u);
-                    }
-                    const float c = sA[ai] - sB[cen];
-                    c4[t] = (fixed_ok && k >= klo && k <= khi) ? c : 2.f;
-                }
-            }
-            st_stream(vol + (((size_t)v * H + y) * W + j) * Lp + 64 * E, f32x4{c4[0], c4[1], c4[2], c4[3]});
-        }
+    // slices whose lane labels are all real (config B: 192 of 193) keep no padding offsets
+    // live in registers
+    if (kb + 64 * E <= L) {
+        if (v == 0) walk(IC<0>{}, IC<0>{});
+        else walk(IC<1>{}, IC<0>{});
+    } else {
+        if (v == 0) walk(IC<0>{}, IC<1>{});
+        else walk(IC<1>{}, IC<1>{});
     }
 }
 
@@ -561,7 +581,7 @@ static int cost_lanes(const DevParams& P) {
 size_t cost_volume_lds_bytes(const DevParams& P) {
     const int E = cost_lanes(P);
     const int G = (E & 1) ? 2 * E : E;
-    return (size_t)(CW_THREADS / 64) * 2 * cost_stage_slots(CW_SEG, G) * 64;
+    return (size_t)(CW_THREADS / 64) * (2 * cost_stage_slots(CW_SEG, G) * 64 + CW_SEG * 16);
 }
 
 template <int E, bool HSI, bool MASK>

@@ -38,11 +38,17 @@ __global__ __launch_bounds__(TPB) void k_copy(const f4* __restrict__ src, f4* __
 
 template <bool NT>
 __global__ __launch_bounds__(TPB) void k_fill(f4* __restrict__ dst, size_t n4, float x) {
-    const size_t stride = (size_t)gridDim.x * TPB;
-    for (size_t i = (size_t)blockIdx.x * TPB + threadIdx.x; i < n4; i += stride) {
-        const f4 v = f4{x, x, x, x};
-        if (NT) __builtin_nontemporal_store(v, dst + i);
-        else dst[i] = v;
+    const size_t stride = (size_t)gridDim.x * TPB * UNR;
+    const f4 v = f4{x, x, x, x};
+    for (size_t base = (size_t)blockIdx.x * TPB * UNR + threadIdx.x; base < n4; base += stride) {
+#pragma unroll
+        for (int u = 0; u < UNR; ++u) {  // UNR independent 16-B stores in flight per lane
+            const size_t i = base + (size_t)u * TPB;
+            if (i < n4) {
+                if (NT) __builtin_nontemporal_store(v, dst + i);
+                else dst[i] = v;
+            }
+        }
     }
 }
 
