@@ -129,6 +129,13 @@ def load() -> ctypes.CDLL:
         raise ImportError(
             f"{path} not found: build the gfx950 library first "
             "(`make lib` or `python -c 'import __graft_entry__ as g; g.build()'`)")
+    # One HIP runtime per process: torch ships its own libamdhip64 (same soname).  Loaded
+    # first, it is the copy the library's DT_NEEDED binds to; loaded after ours, torch
+    # would start a second runtime that sees no device.
+    try:
+        import torch  # noqa: F401
+    except ImportError:
+        pass
     lib = ctypes.CDLL(path)
     for name, (res, args) in {**SIGNATURES, **OPS_SIGNATURES}.items():
         fn = getattr(lib, name)

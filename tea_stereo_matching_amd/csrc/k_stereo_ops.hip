@@ -37,14 +37,50 @@ __device__ __forceinline__ uint32_t cast_u8_x86(float t) {
     return (t > -2147483648.0f && t < 2147483648.0f) ? ((uint32_t)(int32_t)t & 0xffu) : 0u;
 }
 
-// grid over (row, group of 4 pixels); returns false past the row end
-struct RowGrid {
-    int y, x0;
+// Pixel groups: 4 consecutive pixels of a row per lane, the (row, group) pairs of a map
+// flattened over blockIdx.x (no idle lanes at the row ends).  Dense maps (rows packed
+// back to back, every map of the call) run as one row of rows*cols pixels, so groups never
+// straddle a misaligned row start and the loads / stores are whole vectors.
+struct Grp {
+    int y, x0, n;  // row, first pixel, pixels in the group (0: past the map)
 };
-__device__ __forceinline__ RowGrid row_grid(int cols) {
-    const int groups = (cols + OPS_PX - 1) / OPS_PX;
-    const int g = blockIdx.x * blockDim.x + threadIdx.x;
-    return RowGrid{(int)blockIdx.y, g < groups ? g * OPS_PX : cols};
+__device__ __forceinline__ Grp pixel_group(int rows, int cols) {
+    const int gpr = (cols + OPS_PX - 1) / OPS_PX;
+    const long t = (long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= (long)rows * gpr) return Grp{0, 0, 0};
+    const int y = (int)(t / gpr);
+    const int x0 = (int)(t - (long)y * gpr) * OPS_PX;
+    return Grp{y, x0, min(OPS_PX, cols - x0)};
+}
+
+typedef float f2v __attribute__((ext_vector_type(2)));
+typedef float f4v __attribute__((ext_vector_type(4)));
+
+// the group's n <= 4 floats at s: two 8-B loads when whole and 8-B aligned
+__device__ __forceinline__ void load4(const float* __restrict__ s, int n, float (&v)[OPS_PX]) {
+    if (n == OPS_PX && ((uintptr_t)s & 7) == 0) {
+        const f2v a = reinterpret_cast<const f2v*>(s)[0], b = reinterpret_cast<const f2v*>(s)[1];
+        v[0] = a.x; v[1] = a.y; v[2] = b.x; v[3] = b.y;
+        return;
+    }
+#pragma unroll
+    for (int k = 0; k < OPS_PX; ++k) v[k] = k < n ? s[k] : 0.f;
+}
+
+// n <= 4 groups of 3 floats (12 n bytes) at d: 16-B / 8-B vectors when whole and aligned
+__device__ __forceinline__ void store4x3(float* __restrict__ d, int n, const float (&o)[3 * OPS_PX]) {
+    if (n == OPS_PX && ((uintptr_t)d & 15) == 0) {
+#pragma unroll
+        for (int i = 0; i < 3; ++i)
+            reinterpret_cast<f4v*>(d)[i] = f4v{o[4 * i], o[4 * i + 1], o[4 * i + 2], o[4 * i + 3]};
+        return;
+    }
+    if (n == OPS_PX && ((uintptr_t)d & 7) == 0) {
+#pragma unroll
+        for (int i = 0; i < 6; ++i) reinterpret_cast<f2v*>(d)[i] = f2v{o[2 * i], o[2 * i + 1]};
+        return;
+    }
+    for (int i = 0; i < 3 * n; ++i) d[i] = o[i];
 }
 
 // ---- f2 ---------------------------------------------------------------------------
@@ -80,23 +116,48 @@ __device__ __forceinline__ void block_minmax(uint32_t& lo, int& hi, uint32_t* s_
     }
 }
 
-// part: MM_BLOCKS partial pairs per map (map z at part + 2 * MM_BLOCKS * z)
+// part: MM_BLOCKS partial pairs per map (map z at part + 2 * MM_BLOCKS * z); a grid-stride
+// walk over the map's pixel groups, two groups in flight per lane
 __global__ void k_minmax(Tab<const float> srcs, int rows, int cols, size_t step_f, uint32_t* __restrict__ part) {
     __shared__ uint32_t s_lo[16];
     __shared__ int s_hi[16];
     const float* __restrict__ src = srcs.p[blockIdx.z];
     part += (size_t)2 * MM_BLOCKS * blockIdx.z;
-    const int n = rows * cols;
+    const int gpr = (cols + OPS_PX - 1) / OPS_PX;
+    const long ng = (long)rows * gpr, stride = (long)gridDim.x * blockDim.x;
     uint32_t lo = 0x7f800000u;
     int hi = (int)0xff800000u;  // -inf: no valid pixel
-    for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
-        const int y = i / cols, x = i - y * cols;
-        const float v = src[(size_t)y * step_f + x];
-        if (v >= 0.f && v != __int_as_float(0x7f800000)) {
-            const uint32_t b = __float_as_uint(v + 0.f);
-            lo = min(lo, b);
-            hi = max(hi, (int)b);
-        }
+    auto fold = [&](const float (&v)[OPS_PX], int n) {
+#pragma unroll
+        for (int k = 0; k < OPS_PX; ++k)
+            if (k < n && v[k] >= 0.f && v[k] != __int_as_float(0x7f800000)) {
+                const uint32_t b = __float_as_uint(v[k] + 0.f);
+                lo = min(lo, b);
+                hi = max(hi, (int)b);
+            }
+    };
+    auto at = [&](long t, int& n) {
+        const int y = (int)(t / gpr), x0 = (int)(t - (long)y * gpr) * OPS_PX;
+        n = min(OPS_PX, cols - x0);
+        return src + (size_t)y * step_f + x0;
+    };
+    long t = (long)blockIdx.x * blockDim.x + threadIdx.x;
+    for (; t + stride < ng; t += 2 * stride) {
+        int n0, n1;
+        const float* s0 = at(t, n0);
+        const float* s1 = at(t + stride, n1);
+        float v0[OPS_PX], v1[OPS_PX];
+        load4(s0, n0, v0);
+        load4(s1, n1, v1);
+        fold(v0, n0);
+        fold(v1, n1);
+    }
+    if (t < ng) {
+        int n0;
+        const float* s0 = at(t, n0);
+        float v0[OPS_PX];
+        load4(s0, n0, v0);
+        fold(v0, n0);
     }
     block_minmax(lo, hi, s_lo, s_hi);
     if (threadIdx.x == 0) {
@@ -127,28 +188,36 @@ __global__ void k_minmax_final(uint32_t* __restrict__ part, int nparts, uint32_t
 __global__ void k_colormap(Tab<const float> srcs, int rows, int cols, size_t step_f,
                            const uint32_t* __restrict__ mm, int use_range, float rmin, float rmax,
                            Lut lut, Tab<uint8_t> dsts, size_t dstep) {
-    const RowGrid p = row_grid(cols);
-    if (p.x0 >= cols) return;
+    const Grp p = pixel_group(rows, cols);
+    if (p.n == 0) return;
     const float* __restrict__ src = srcs.p[blockIdx.z];
     uint8_t* __restrict__ dst = dsts.p[blockIdx.z];
     if (!use_range) mm += 2 * blockIdx.z;
     const float mn = use_range ? rmin : __uint_as_float(mm[0]);
     const float mx = use_range ? rmax : __int_as_float((int)mm[1]);
-    const float* s = src + (size_t)p.y * step_f;
     uint8_t* d = dst + (size_t)p.y * dstep + 3 * (size_t)p.x0;
-    const int n = min(OPS_PX, cols - p.x0);
+    const int n = p.n;
+    float v[OPS_PX];
+    load4(src + (size_t)p.y * step_f + p.x0, n, v);
     uint32_t c[OPS_PX];
 #pragma unroll
     for (int k = 0; k < OPS_PX; ++k) {
-        const float v = k < n ? s[p.x0 + k] : 0.f;
-        const bool black = use_range ? (v < mn || v > mx) : (v < 0.f);
-        c[k] = black ? 0u : lut.bgr[cast_u8_x86(((v - mn) / (mx - mn)) * 255)];
+        const bool black = use_range ? (v[k] < mn || v[k] > mx) : (v[k] < 0.f);
+        c[k] = black ? 0u : lut.bgr[cast_u8_x86(((v[k] - mn) / (mx - mn)) * 255)];
     }
     if (n == OPS_PX && ((uintptr_t)d & 3) == 0) {  // 12 B: three dword stores
         uint32_t* d4 = reinterpret_cast<uint32_t*>(d);
         d4[0] = c[0] | (c[1] << 24);
         d4[1] = (c[1] >> 8) | (c[2] << 16);
         d4[2] = (c[2] >> 16) | (c[3] << 8);
+    } else if (n == OPS_PX && ((uintptr_t)d & 1) == 0) {  // 2-B aligned: six halfword stores
+        uint16_t* d2 = reinterpret_cast<uint16_t*>(d);
+        d2[0] = (uint16_t)c[0];
+        d2[1] = (uint16_t)((c[0] >> 16) | (c[1] << 8));
+        d2[2] = (uint16_t)(c[1] >> 8);
+        d2[3] = (uint16_t)c[2];
+        d2[4] = (uint16_t)((c[2] >> 16) | (c[3] << 8));
+        d2[5] = (uint16_t)(c[3] >> 8);
     } else {
         for (int k = 0; k < n; ++k) {
             d[3 * k + 0] = (uint8_t)c[k];
@@ -162,67 +231,94 @@ __global__ void k_colormap(Tab<const float> srcs, int rows, int cols, size_t ste
 
 __global__ void k_depth(Tab<const float> srcs, int rows, int cols, size_t step_f, float fb,
                         Tab<float> dsts, size_t dstep_f) {
-    const RowGrid p = row_grid(cols);
-    if (p.x0 >= cols) return;
+    const Grp p = pixel_group(rows, cols);
+    if (p.n == 0) return;
     const float* __restrict__ src = srcs.p[blockIdx.z];
-    float* __restrict__ dst = dsts.p[blockIdx.z];
-    const int n = min(OPS_PX, cols - p.x0);
-    for (int k = 0; k < n; ++k) {
-        const float d = src[(size_t)p.y * step_f + p.x0 + k];
-        dst[(size_t)p.y * dstep_f + p.x0 + k] = (d < 0.f || isinf(d)) ? 0.f : fb / d;
+    float* __restrict__ d = dsts.p[blockIdx.z] + (size_t)p.y * dstep_f + p.x0;
+    float v[OPS_PX];
+    load4(src + (size_t)p.y * step_f + p.x0, p.n, v);
+#pragma unroll
+    for (int k = 0; k < OPS_PX; ++k) v[k] = (v[k] < 0.f || isinf(v[k])) ? 0.f : fb / v[k];
+    if (p.n == OPS_PX && ((uintptr_t)d & 7) == 0) {
+        reinterpret_cast<f2v*>(d)[0] = f2v{v[0], v[1]};
+        reinterpret_cast<f2v*>(d)[1] = f2v{v[2], v[3]};
+    } else {
+        for (int k = 0; k < p.n; ++k) d[k] = v[k];
     }
 }
 
-struct F3 {
-    float x, y, z;
-};
+// image coordinates of the group's first pixel: a dense map runs as one row of rows*cols
+// pixels, wcols is the image width (= cols for a strided map, which has y = the row)
+__device__ __forceinline__ void group_uv(const Grp& p, int wcols, int& u, int& v) {
+    const int i = p.x0;  // dense: flat pixel index (y = 0)
+    v = p.y + i / wcols;
+    u = i - (i / wcols) * wcols;
+}
 
-__global__ void k_xyz(Tab<const float> srcs, int rows, int cols, size_t step_f, float f,
+__global__ void k_xyz(Tab<const float> srcs, int rows, int cols, size_t step_f, int wcols, float f,
                       float fb, float cx, float cy, Tab<float> dsts, size_t dstep_f) {
-    const RowGrid p = row_grid(cols);
-    if (p.x0 >= cols) return;
+    const Grp p = pixel_group(rows, cols);
+    if (p.n == 0) return;
     const float* __restrict__ src = srcs.p[blockIdx.z];
-    float* __restrict__ dst = dsts.p[blockIdx.z];
-    const int n = min(OPS_PX, cols - p.x0);
-    const float v = (float)p.y;
-    for (int k = 0; k < n; ++k) {
-        const int u = p.x0 + k;
-        const float d = src[(size_t)p.y * step_f + u];
-        F3 o{0.f, 0.f, 0.f};
-        if (!(d < 0.f || isinf(d))) {
-            const float Z = fb / d;
+    float* __restrict__ d = dsts.p[blockIdx.z] + (size_t)p.y * dstep_f + 3 * (size_t)p.x0;
+    float dv[OPS_PX];
+    load4(src + (size_t)p.y * step_f + p.x0, p.n, dv);
+    int u, v;
+    group_uv(p, wcols, u, v);
+    float o[3 * OPS_PX];
+#pragma unroll
+    for (int k = 0; k < OPS_PX; ++k) {
+        o[3 * k] = o[3 * k + 1] = o[3 * k + 2] = 0.f;
+        if (!(dv[k] < 0.f || isinf(dv[k]))) {
+            const float Z = fb / dv[k];
             const float Zf = Z / f;
-            o = F3{((float)u - cx) * Zf, (v - cy) * Zf, Z};
+            o[3 * k] = ((float)u - cx) * Zf;
+            o[3 * k + 1] = ((float)v - cy) * Zf;
+            o[3 * k + 2] = Z;
         }
-        *reinterpret_cast<F3*>(dst + (size_t)p.y * dstep_f + 3 * (size_t)u) = o;
+        if (++u == wcols) {  // next pixel: the row wraps (dense maps)
+            u = 0;
+            ++v;
+        }
     }
+    store4x3(d, p.n, o);
 }
 
 struct Q16 {
     float q[16];
 };
 
-__global__ void k_xyz_q(Tab<const float> srcs, int rows, int cols, size_t step_f, Q16 Q,
+__global__ void k_xyz_q(Tab<const float> srcs, int rows, int cols, size_t step_f, int wcols, Q16 Q,
                         Tab<float> dsts, size_t dstep_f) {
-    const RowGrid p = row_grid(cols);
-    if (p.x0 >= cols) return;
+    const Grp p = pixel_group(rows, cols);
+    if (p.n == 0) return;
     const float* __restrict__ src = srcs.p[blockIdx.z];
-    float* __restrict__ dst = dsts.p[blockIdx.z];
-    const int n = min(OPS_PX, cols - p.x0);
-    for (int k = 0; k < n; ++k) {
-        const int u = p.x0 + k;
-        const float pv[4] = {(float)u, (float)p.y, src[(size_t)p.y * step_f + u], 1.f};
+    float* __restrict__ d = dsts.p[blockIdx.z] + (size_t)p.y * dstep_f + 3 * (size_t)p.x0;
+    float dv[OPS_PX];
+    load4(src + (size_t)p.y * step_f + p.x0, p.n, dv);
+    int u, v;
+    group_uv(p, wcols, u, v);
+    float o[3 * OPS_PX];
+#pragma unroll
+    for (int k = 0; k < OPS_PX; ++k) {
+        const float pv[4] = {(float)u, (float)v, dv[k], 1.f};
         float r[4];
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
-            float s = 0.f;
+            float sacc = 0.f;
 #pragma unroll
-            for (int j = 0; j < 4; ++j) s += Q.q[4 * i + j] * pv[j];
-            r[i] = s;
+            for (int j = 0; j < 4; ++j) sacc += Q.q[4 * i + j] * pv[j];
+            r[i] = sacc;
         }
-        *reinterpret_cast<F3*>(dst + (size_t)p.y * dstep_f + 3 * (size_t)u) =
-            F3{r[0] / r[3], r[1] / r[3], r[2] / r[3]};
+        o[3 * k] = r[0] / r[3];
+        o[3 * k + 1] = r[1] / r[3];
+        o[3 * k + 2] = r[2] / r[3];
+        if (++u == wcols) {
+            u = 0;
+            ++v;
+        }
     }
+    store4x3(d, p.n, o);
 }
 
 // ---- f4 ---------------------------------------------------------------------------
@@ -296,18 +392,35 @@ __global__ void k_remap_fixed(Tab<const uint8_t> srcs, int sh, int sw, size_t ss
                               const int16_t* __restrict__ xy, size_t xy_step_e,
                               const uint16_t* __restrict__ fxy, size_t fxy_step_e, int rows, int cols,
                               Tab<uint8_t> dsts, size_t dstep) {
-    const RowGrid p = row_grid(cols);
-    if (p.x0 >= cols) return;
+    const Grp p = pixel_group(rows, cols);
+    if (p.n == 0) return;
     const uint8_t* __restrict__ src = srcs.p[blockIdx.z];
     uint8_t* __restrict__ dst = dsts.p[blockIdx.z];
-    const int n = min(OPS_PX, cols - p.x0);
+    const int n = p.n;
+    // the group's map entries: 16 B of (x, y) pairs and 8 B of fractions, as two vector
+    // loads when whole and aligned
+    const int16_t* xr = xy + (size_t)p.y * xy_step_e + 2 * (size_t)p.x0;
+    const uint16_t* fr = fxy + (size_t)p.y * fxy_step_e + p.x0;
+    uint32_t mxy[OPS_PX], mf[OPS_PX];
+    if (n == OPS_PX && ((uintptr_t)xr & 15) == 0 && ((uintptr_t)fr & 7) == 0) {
+        const uint4 a = *reinterpret_cast<const uint4*>(xr);
+        const uint2 b = *reinterpret_cast<const uint2*>(fr);
+        mxy[0] = a.x; mxy[1] = a.y; mxy[2] = a.z; mxy[3] = a.w;
+        mf[0] = b.x; mf[1] = b.x >> 16; mf[2] = b.y; mf[3] = b.y >> 16;
+    } else {
+#pragma unroll
+        for (int k = 0; k < OPS_PX; ++k) {
+            const int kk = k < n ? k : n - 1;
+            mxy[k] = (uint32_t)(uint16_t)xr[2 * kk] | ((uint32_t)(uint16_t)xr[2 * kk + 1] << 16);
+            mf[k] = fr[kk];
+        }
+    }
     uint32_t o[OPS_PX][C];
 #pragma unroll
     for (int k = 0; k < OPS_PX; ++k) {
-        const int x = min(p.x0 + k, cols - 1);
-        const int sx = xy[(size_t)p.y * xy_step_e + 2 * (size_t)x];
-        const int sy = xy[(size_t)p.y * xy_step_e + 2 * (size_t)x + 1];
-        const int f = fxy[(size_t)p.y * fxy_step_e + x] & 1023;
+        const int sx = (int)(int16_t)(mxy[k] & 0xffffu);
+        const int sy = (int)(int16_t)(mxy[k] >> 16);
+        const int f = (int)(mf[k] & 1023u);
         remap_px<C>(src, sh, sw, sstep, sx, sy, f & 31, f >> 5, o[k]);
     }
     store_px<C>(dst + (size_t)p.y * dstep + (size_t)p.x0 * C, n, o);
@@ -324,11 +437,11 @@ __global__ void k_remap_float(Tab<const uint8_t> srcs, int sh, int sw, size_t ss
                               const float* __restrict__ mapx, const float* __restrict__ mapy,
                               size_t map_step_f, int rows, int cols, Tab<uint8_t> dsts,
                               size_t dstep) {
-    const RowGrid p = row_grid(cols);
-    if (p.x0 >= cols) return;
+    const Grp p = pixel_group(rows, cols);
+    if (p.n == 0) return;
     const uint8_t* __restrict__ src = srcs.p[blockIdx.z];
     uint8_t* __restrict__ dst = dsts.p[blockIdx.z];
-    const int n = min(OPS_PX, cols - p.x0);
+    const int n = p.n;
     uint32_t o[OPS_PX][C];
 #pragma unroll
     for (int k = 0; k < OPS_PX; ++k) {
@@ -343,9 +456,22 @@ __global__ void k_remap_float(Tab<const uint8_t> srcs, int sh, int sw, size_t ss
 
 // ---- host side --------------------------------------------------------------------
 
+// the flattened (row, pixel group) grid of pixel_group(), n maps
 dim3 row_blocks(int rows, int cols, int n = 1) {
-    const int groups = (cols + OPS_PX - 1) / OPS_PX;
-    return dim3((groups + OPS_THREADS - 1) / OPS_THREADS, rows, n);
+    const long groups = (long)rows * ((cols + OPS_PX - 1) / OPS_PX);
+    return dim3((unsigned)((groups + OPS_THREADS - 1) / OPS_THREADS), 1, n);
+}
+
+// A map whose rows are packed (step = row bytes, input and output) runs as one row of
+// rows * cols pixels: rows -> 1, cols -> rows * cols (the f3 kernels keep the true width
+// for the pixel coordinates).
+struct Shape {
+    int rows, cols;
+};
+Shape dense_shape(int rows, int cols, size_t step, size_t in_bpp, size_t out_step, size_t out_bpp) {
+    if (step == in_bpp * cols && out_step == out_bpp * cols && (long)rows * cols <= 0x7fffffffL)
+        return Shape{1, rows * cols};
+    return Shape{rows, cols};
 }
 
 template <class T, class U>
@@ -439,17 +565,18 @@ int colormap_launch(const Tab<const float>& src, int nm, int rows, int cols, siz
                     uint32_t* scratch, hipStream_t st) {
     const Lut L = make_lut(lut768);
     uint32_t* mm = scratch;
+    const Shape sh = dense_shape(rows, cols, step, 4, out_step, 3);
     if (!use_range) {
-        const int n = rows * cols;
-        // fewer partial blocks per map when the launch carries many maps (the chip is full)
-        const int per_map = max(8, MM_BLOCKS / nm);
-        const int blocks = min((n + OPS_THREADS - 1) / OPS_THREADS, per_map);
-        hipLaunchKernelGGL(k_minmax, dim3(blocks, 1, nm), dim3(OPS_THREADS), 0, st, src, rows, cols, step / 4,
-                           mm + 2 * kOpsBatch);
+        const long groups = (long)rows * ((cols + OPS_PX - 1) / OPS_PX);
+        // about 2048 partial blocks a launch (8 a CU), at most MM_BLOCKS per map
+        const int per_map = min(MM_BLOCKS, max(8, 2048 / nm));
+        const int blocks = (int)min((groups + OPS_THREADS - 1) / OPS_THREADS, (long)per_map);
+        hipLaunchKernelGGL(k_minmax, dim3(blocks, 1, nm), dim3(OPS_THREADS), 0, st, src, sh.rows, sh.cols,
+                           step / 4, mm + 2 * kOpsBatch);
         hipLaunchKernelGGL(k_minmax_final, dim3(1, 1, nm), dim3(1024), 0, st, mm + 2 * kOpsBatch, blocks, mm);
     }
-    hipLaunchKernelGGL(k_colormap, row_blocks(rows, cols, nm), dim3(OPS_THREADS), 0, st, src, rows, cols,
-                       step / 4, mm, use_range, min_val, max_val, L, dst, out_step);
+    hipLaunchKernelGGL(k_colormap, row_blocks(sh.rows, sh.cols, nm), dim3(OPS_THREADS), 0, st, src, sh.rows,
+                       sh.cols, step / 4, mm, use_range, min_val, max_val, L, dst, out_step);
     return status(hipGetLastError());
 }
 
@@ -539,10 +666,8 @@ int tsm_reproject_to_depth_device(const float* d_disp, int rows, int cols, size_
     if (!d_disp || !d_depth || bad_dims(rows, cols) || step % 4 || out_step % 4 ||
         step < 4 * (size_t)cols || out_step < 4 * (size_t)cols)
         return TSM_ERR_ARGUMENT;
-    hipLaunchKernelGGL(k_depth, row_blocks(rows, cols), dim3(OPS_THREADS), 0, (hipStream_t)hip_stream,
-                       tab_one<const float>(d_disp), rows, cols, step / 4, focal * baseline,
-                       tab_one<float>(d_depth), out_step / 4);
-    return status(hipGetLastError());
+    return tsm_reproject_to_depth_batch_device(1, &d_disp, rows, cols, step, focal, baseline, &d_depth, out_step,
+                                               hip_stream);
 }
 
 int tsm_reproject_to_depth_batch_device(int n, const float* const* d_disps, int rows, int cols, size_t step,
@@ -551,10 +676,11 @@ int tsm_reproject_to_depth_batch_device(int n, const float* const* d_disps, int 
     if (n < 0 || (n > 0 && (null_in((const void* const*)d_disps, n) || null_in((const void* const*)d_depths, n))) ||
         bad_dims(rows, cols) || step % 4 || out_step % 4 || step < 4 * (size_t)cols || out_step < 4 * (size_t)cols)
         return TSM_ERR_ARGUMENT;
+    const Shape sh = dense_shape(rows, cols, step, 4, out_step, 4);
     for (int i = 0; i < n; i += kOpsBatch) {
         const int k = min(kOpsBatch, n - i);
-        hipLaunchKernelGGL(k_depth, row_blocks(rows, cols, k), dim3(OPS_THREADS), 0, (hipStream_t)hip_stream,
-                           tab_of<const float>(d_disps + i, k), rows, cols, step / 4, focal * baseline,
+        hipLaunchKernelGGL(k_depth, row_blocks(sh.rows, sh.cols, k), dim3(OPS_THREADS), 0, (hipStream_t)hip_stream,
+                           tab_of<const float>(d_disps + i, k), sh.rows, sh.cols, step / 4, focal * baseline,
                            tab_of<float>(d_depths + i, k), out_step / 4);
     }
     return status(hipGetLastError());
@@ -578,10 +704,8 @@ int tsm_reproject_to_3d_device(const float* d_disp, int rows, int cols, size_t s
     if (!d_disp || !d_xyz || bad_dims(rows, cols) || step % 4 || out_step % 4 ||
         step < 4 * (size_t)cols || out_step < 12 * (size_t)cols)
         return TSM_ERR_ARGUMENT;
-    hipLaunchKernelGGL(k_xyz, row_blocks(rows, cols), dim3(OPS_THREADS), 0, (hipStream_t)hip_stream,
-                       tab_one<const float>(d_disp), rows, cols, step / 4, focal, focal * baseline, cx, cy,
-                       tab_one<float>(d_xyz), out_step / 4);
-    return status(hipGetLastError());
+    return tsm_reproject_to_3d_batch_device(1, &d_disp, rows, cols, step, focal, baseline, cx, cy, &d_xyz,
+                                            out_step, hip_stream);
 }
 
 int tsm_reproject_to_3d_batch_device(int n, const float* const* d_disps, int rows, int cols, size_t step,
@@ -590,11 +714,12 @@ int tsm_reproject_to_3d_batch_device(int n, const float* const* d_disps, int row
     if (n < 0 || (n > 0 && (null_in((const void* const*)d_disps, n) || null_in((const void* const*)d_xyzs, n))) ||
         bad_dims(rows, cols) || step % 4 || out_step % 4 || step < 4 * (size_t)cols || out_step < 12 * (size_t)cols)
         return TSM_ERR_ARGUMENT;
+    const Shape sh = dense_shape(rows, cols, step, 4, out_step, 12);
     for (int i = 0; i < n; i += kOpsBatch) {
         const int k = min(kOpsBatch, n - i);
-        hipLaunchKernelGGL(k_xyz, row_blocks(rows, cols, k), dim3(OPS_THREADS), 0, (hipStream_t)hip_stream,
-                           tab_of<const float>(d_disps + i, k), rows, cols, step / 4, focal, focal * baseline, cx,
-                           cy, tab_of<float>(d_xyzs + i, k), out_step / 4);
+        hipLaunchKernelGGL(k_xyz, row_blocks(sh.rows, sh.cols, k), dim3(OPS_THREADS), 0, (hipStream_t)hip_stream,
+                           tab_of<const float>(d_disps + i, k), sh.rows, sh.cols, step / 4, cols, focal,
+                           focal * baseline, cx, cy, tab_of<float>(d_xyzs + i, k), out_step / 4);
     }
     return status(hipGetLastError());
 }
@@ -618,8 +743,10 @@ int tsm_reproject_to_3d_q_device(const float* d_disp, int rows, int cols, size_t
         return TSM_ERR_ARGUMENT;
     Q16 Q;
     for (int i = 0; i < 16; ++i) Q.q[i] = (float)q16[i];  // Q.convertTo(CV_32F), stereo.cpp:190
-    hipLaunchKernelGGL(k_xyz_q, row_blocks(rows, cols), dim3(OPS_THREADS), 0, (hipStream_t)hip_stream,
-                       tab_one<const float>(d_disp), rows, cols, step / 4, Q, tab_one<float>(d_xyz), out_step / 4);
+    const Shape sh = dense_shape(rows, cols, step, 4, out_step, 12);
+    hipLaunchKernelGGL(k_xyz_q, row_blocks(sh.rows, sh.cols), dim3(OPS_THREADS), 0, (hipStream_t)hip_stream,
+                       tab_one<const float>(d_disp), sh.rows, sh.cols, step / 4, cols, Q, tab_one<float>(d_xyz),
+                       out_step / 4);
     return status(hipGetLastError());
 }
 
@@ -659,14 +786,18 @@ int tsm_remap_linear_fixed_batch_device(int n, const uint8_t* const* d_srcs, int
         xy_step < 4 * (size_t)cols || fxy_step < 2 * (size_t)cols || dst_step < (size_t)C * cols)
         return TSM_ERR_ARGUMENT;
     hipStream_t st = (hipStream_t)hip_stream;
+    // packed maps and output run as one row (the source is addressed through the maps)
+    const bool dense = xy_step == 4 * (size_t)cols && fxy_step == 2 * (size_t)cols && dst_step == (size_t)C * cols &&
+                       (long)rows * cols <= 0x7fffffffL;
+    const int rr = dense ? 1 : rows, cc = dense ? rows * cols : cols;
     for (int i = 0; i < n; i += kOpsBatch) {
         const int k = min(kOpsBatch, n - i);
-        const dim3 g = row_blocks(rows, cols, k);
+        const dim3 g = row_blocks(rr, cc, k);
         const Tab<const uint8_t> s = tab_of<const uint8_t>(d_srcs + i, k);
         const Tab<uint8_t> d = tab_of<uint8_t>(d_dsts + i, k);
 #define TSM_REMAP_FIXED(CC)                                                                               \
         hipLaunchKernelGGL(k_remap_fixed<CC>, g, dim3(OPS_THREADS), 0, st, s, src_rows, src_cols, src_step, \
-                           d_xy, xy_step / 2, d_fxy, fxy_step / 2, rows, cols, d, dst_step)
+                           d_xy, xy_step / 2, d_fxy, fxy_step / 2, rr, cc, d, dst_step)
         if (C == 1) TSM_REMAP_FIXED(1);
         else if (C == 3) TSM_REMAP_FIXED(3);
         else TSM_REMAP_FIXED(4);

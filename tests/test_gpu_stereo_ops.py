@@ -249,3 +249,48 @@ def test_group_forms_reject_bad_tables(tsm):
     assert lib.tsm_apply_colormap_batch_device(2, two_null, 4, 4, 16, None, 0, 0.0, 0.0, two_null, 12, None) == N.TSM_ERR_ARGUMENT
     assert lib.tsm_reproject_to_depth_batch_device(-1, None, 4, 4, 16, 1.0, 1.0, None, 16, None) == N.TSM_ERR_ARGUMENT
     assert lib.tsm_reproject_to_depth_batch_device(0, None, 4, 4, 16, 1.0, 1.0, None, 16, None) == N.TSM_OK
+
+
+def test_strided_and_offset_maps(tsm, oracle):
+    """The kernels' two layouts: packed maps (run as one flat row, vector loads / stores)
+    and strided ones (padded rows, maps at 4-B but not 8-B aligned offsets: scalar and
+    halfword paths), every result equal to the oracle's."""
+    import torch
+    from tea_stereo_matching_amd import _native as N
+
+    lib = N.load()
+    P = ctypes.c_void_p
+    rng = np.random.default_rng(31)
+    H, W, n = 29, 53, 5
+    ds = [_disp(rng, H, W) for _ in range(n)]
+    # maps packed back to back in one buffer from element 1 on: odd maps start 4-B aligned only
+    flat = torch.zeros(1 + n * H * W, dtype=torch.float32, device="cuda")
+    packed = [flat[1 + i * H * W: 1 + (i + 1) * H * W].view(H, W) for i in range(n)]
+    # strided: rows padded to W + 3 floats
+    pad = torch.zeros(n, H, W + 3, dtype=torch.float32, device="cuda")
+    strided = [pad[i, :, :W] for i in range(n)]
+    for i, d in enumerate(ds):
+        packed[i].copy_(torch.from_numpy(d))
+        strided[i].copy_(torch.from_numpy(d))
+    lut = tsm.JETColorMap()
+    lp = lut.ctypes.data_as(P)
+    arr = lambda ts: (P * len(ts))(*[t.data_ptr() for t in ts])  # noqa: E731
+    for src, step in ((packed, 4 * W), (strided, 4 * (W + 3))):
+        # outputs: packed from a 2-B offset (colour), padded rows (depth / points)
+        cbuf = torch.zeros(2 + n * H * W * 3, dtype=torch.uint8, device="cuda")
+        cols = [cbuf[2 + i * H * W * 3: 2 + (i + 1) * H * W * 3] for i in range(n)]
+        dep = torch.zeros(n, H, W + 1, dtype=torch.float32, device="cuda")
+        xyz = torch.zeros(n, H, 3 * W + 2, dtype=torch.float32, device="cuda")
+        assert lib.tsm_apply_colormap_batch_device(n, arr(src), H, W, step, lp, 0, 0.0, 0.0, arr(cols), 3 * W,
+                                                   None) == 0
+        assert lib.tsm_reproject_to_depth_batch_device(n, arr(src), H, W, step, 700.0, 0.5, arr(list(dep)),
+                                                       4 * (W + 1), None) == 0
+        assert lib.tsm_reproject_to_3d_batch_device(n, arr(src), H, W, step, 700.0, 0.5, 20.0, 11.0,
+                                                    arr(list(xyz)), 4 * (3 * W + 2), None) == 0
+        assert lib.tsm_stream_synchronize(None) == 0
+        for i, d in enumerate(ds):
+            assert np.array_equal(cols[i].cpu().numpy().reshape(H, W, 3), oracle.apply_colormap_ex(d)), (step, i)
+            assert np.array_equal(dep[i, :, :W].cpu().numpy(), oracle.reproject_to_depth(d, 700.0, 0.5),
+                                  equal_nan=True), (step, i)
+            assert np.array_equal(xyz[i, :, :3 * W].cpu().numpy().reshape(H, W, 3),
+                                  oracle.reproject_to_3d(d, 700.0, 0.5, 20.0, 11.0), equal_nan=True), (step, i)
