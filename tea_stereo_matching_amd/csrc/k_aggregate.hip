@@ -870,11 +870,8 @@ int launch_aggregation_pass(float* vol, const uint32_t* arms, const int32_t* ws,
     }();
     const int G = S.nl < ncu ? S.nl : ncu;
     // fused pass pairs: the role-split streamer (v6); single passes: v5 where its rings fit
-#ifdef TSM_EXP_V6_SINGLE  // experiment build: single passes through the split streamer too
-    const bool v5_fits = false;
-#else
+    // (v6 for single passes too measured 1 % fewer pairs/s: round 3, same box)
     const bool v5_fits = !fused && Q <= 64 && !big && agg_stream_lds(P, false) <= kLdsBytes;
-#endif
     if (!v5_fits) {
         const size_t slds = agg_split_lds(S.qn0);
         const dim3 sgrid(G, nslice, P.npairs);
