@@ -191,19 +191,6 @@ constexpr int AS_LAG = AS_AH + 1;           // pass B at step s outputs chunk s 
 constexpr int AS_MC = 16;                   // meta ring chunks (> AHEAD + GRP + LAG)
 static_assert(AS_AHEAD % AS_GRP == 0, "turns land on steps NG*k - AHEAD");
 
-// exact a / b for the aggregation's "C /= windowSize" (see above)
-__device__ __forceinline__ f32x4 div_ws(f32x4 a, float b, float y) {
-    const f32x4 q0 = a * y;
-    const f32x4 r = __builtin_elementwise_fma(-q0, f32x4{b, b, b, b}, a);
-    f32x4 q = __builtin_elementwise_fma(r, f32x4{y, y, y, y}, q0);
-    // 0 < a < 2^-40 (never seen in practice) takes the IEEE path; a == 0 is exact above
-    const u32x4 ab = __builtin_bit_cast(u32x4, a) - 1u;  // +0 wraps to 0xffffffff
-    if (__builtin_expect(min(min(ab.x, ab.y), min(ab.z, ab.w)) < 0x2b800000u - 1u, 0)) {
-        q.x = a.x / b; q.y = a.y / b; q.z = a.z / b; q.w = a.w / b;
-    }
-    return q;
-}
-
 // raw buffer resource over p (gfx9 dword3: 32-bit data format, no swizzle); offsets are
 // unsigned 32-bit, the launcher checks that every line of a pass fits
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t make_rsrc(const void* p) {

@@ -61,6 +61,22 @@ __device__ __forceinline__ void st_stream(float* p, f32x4 v) {
     __builtin_nontemporal_store(v, reinterpret_cast<f32x4*>(p));
 }
 
+// Exact a / b for the aggregation's "C /= windowSize" (ADCensus.cpp:743-748): with
+// y = RN(1/b), q0 = a*y, r = fma(-q0, b, a), q = fma(r, y, q0) equals RN(a/b) for every
+// integer b in [1, 6561] and every a in [2^-40, 2^16) (exhaustively checked,
+// tools/micro/div_check.c); 0 < a < 2^-40 (never seen in practice) takes the IEEE path,
+// a == 0 is exact.
+__device__ __forceinline__ f32x4 div_ws(f32x4 a, float b, float y) {
+    const f32x4 q0 = a * y;
+    const f32x4 r = __builtin_elementwise_fma(-q0, f32x4{b, b, b, b}, a);
+    f32x4 q = __builtin_elementwise_fma(r, f32x4{y, y, y, y}, q0);
+    const u32x4 ab = __builtin_bit_cast(u32x4, a) - 1u;  // +0 wraps to 0xffffffff
+    if (__builtin_expect(min(min(ab.x, ab.y), min(ab.z, ab.w)) < 0x2b800000u - 1u, 0)) {
+        q.x = a.x / b; q.y = a.y / b; q.z = a.z / b; q.w = a.w / b;
+    }
+    return q;
+}
+
 // Largest group a launch carries (pointer tables of per-pair user buffers are kernel
 // arguments of this many entries).
 constexpr int kMaxGroup = 64;

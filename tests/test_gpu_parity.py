@@ -113,6 +113,43 @@ WIDE = [
 ]
 
 
+SCAN_STAGES = ("cost_scan", "wta", "outlier", "subpix")
+SCAN_CASES = [
+    # (seed, H, W, minD, maxD, model, roi, mask)
+    (1, 64, 96, 0, 24, 0, False, False),
+    (3, 97, 131, 0, 64, 0, False, False),
+    (4, 80, 120, 5, 40, 0, False, False),
+    (5, 48, 64, 0, 40, 0, False, False),
+    (31, 24, 300, 0, 192, 0, False, False),
+    (34, 22, 290, 0, 192, 1, False, False),
+    (48, 20, 300, 0, 240, 0, False, False),
+    (6, 40, 96, 0, 48, 0, True, False),   # ROI / mask: maxD = W/2 (:339-340)
+    (7, 40, 96, 0, 48, 1, False, True),
+]
+
+
+@pytest.mark.parametrize("case", SCAN_CASES, ids=[f"s{c[0]}_{c[1]}x{c[2]}_d{c[3]}-{c[4]}_m{c[5]}_r{int(c[6])}k{int(c[7])}"
+                                             for c in SCAN_CASES])
+def test_scanline_and_refine_stages_modes(matcher, tsm, oracle, case):
+    """The scanline volumes of both views and the stages after them, in RGB / HSI / ROI /
+    mask mode, with and without the racy-schedule emulation, equal the oracle's."""
+    seed, H, W, mn, mx, model, roi, mask = case
+    left, right = _synthetic(tsm, seed, H, W, mx - mn + 1)
+    if roi or mask:  # black out a border band and a block (ROI / mask rules)
+        for im in (left, right):
+            im[:, :7] = 0
+            im[H // 3: H // 2, W // 2: W // 2 + 9] = 0
+    for omp in (0, 5):
+        d_g, g = _gpu(matcher, tsm, left, right, model, mn, mx, SCAN_STAGES, omp=omp, roi=roi, mask=mask)
+        kw = {"scan_emulate_threads": omp} if omp else {}
+        d_o, o = oracle.compute(left, right, _oracle_params(oracle, model, mn, mx, roi_matching=int(roi),
+                                                           mask_matching=int(mask), **kw), SCAN_STAGES)
+        _assert_stages_equal(g, o, SCAN_STAGES)
+        assert np.array_equal(d_g, d_o, equal_nan=True)
+    matcher.setMatchingStrategy(tsm.ColorModel.RGB)
+    matcher.setOmpEmulation(0)
+
+
 @pytest.mark.parametrize("case", WIDE, ids=[f"s{c[0]}_{c[1]}x{c[2]}_d{c[3]}-{c[4]}_m{c[5]}" for c in WIDE])
 def test_cost_volume_full_label_width(matcher, tsm, oracle, case):
     seed, H, W, mn, mx, model = case
