@@ -336,11 +336,14 @@ __device__ __forceinline__ void row_taps(const uint8_t* __restrict__ src, int sh
     }
     const uint8_t* row = src + (size_t)sy * sstep;
     const long off = (long)sx * C;
-    const long base = off & ~3L;
-    if (sx >= 0 && sx + 1 < sw && base + 12 <= (long)sw * C && (((uintptr_t)(row + base)) & 3) == 0) {
-        const uint32_t* w = reinterpret_cast<const uint32_t*>(row + base);
+    // the dword-aligned 12 B holding the taps (any row alignment), while they stay inside
+    // the image's bytes (the last row's end is the buffer's)
+    const uintptr_t pa = (uintptr_t)(row + off);
+    const uintptr_t a = pa & ~(uintptr_t)3;
+    if (sx >= 0 && sx + 1 < sw && a + 12 - (uintptr_t)src <= (size_t)(sh - 1) * sstep + (size_t)sw * C) {
+        const uint32_t* w = reinterpret_cast<const uint32_t*>(a);
         const uint32_t w0 = w[0], w1 = w[1], w2 = w[2];
-        const uint32_t sh8 = (uint32_t)(off & 3) * 8;
+        const uint32_t sh8 = (uint32_t)(pa & 3) * 8;
         const uint32_t lo = __builtin_amdgcn_alignbit(w1, w0, sh8);
         const uint32_t hi = __builtin_amdgcn_alignbit(w2, w1, sh8);
 #pragma unroll
