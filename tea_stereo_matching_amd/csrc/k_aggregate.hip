@@ -53,30 +53,34 @@ __device__ __forceinline__ int compute_limit(const DevParams& P, uint32_t p, int
     return d - 1;
 }
 
-// arms[v][y][x] = up | down<<8 | left<<16 | right<<24  (computeLimits, :661-683): one
-// thread a pixel, its four walks reading the image through L1/L2.  Arms are short on real
+// arms[v][y][x] = up | down<<8 | left<<16 | right<<24  (computeLimits, :661-683): the
+// four walks of a pixel on four lanes, reading the image through L1/L2.  Arms are short on real
 // scenes (mean 2.1 px), so the walks are a few dependent cached loads; staging row and
 // column tiles with a maxLength1 halo in LDS measured slower (round 3: 0.089 -> 0.161 ms a
 // pair for the stage, the column tile serialising 16 pixels a thread).
 __global__ void k_arms(const uint32_t* __restrict__ img, uint32_t* __restrict__ arms, DevParams Pk) {
     const DevParams P = Pk;  // kernel args -> registers once (no per-use kernarg reloads)
-    const int x = blockIdx.x * blockDim.x + threadIdx.x;
+    // four lanes a pixel, one direction each (0 up, 1 down, 2 left, 3 right): the four
+    // dependent load chains run side by side; the pixel's lane 0 packs and stores
+    const int t = blockIdx.x * blockDim.x + threadIdx.x;
+    const int x = t >> 2, dir = t & 3;
     const int y = blockIdx.y;
     const int v = blockIdx.z & 1;
-    if (x >= P.W) return;
     pair_shift(blockIdx.z >> 1, P.pstride, img, arms);
     const int W = P.W;
+    const bool inside = x < W;
+    const int xc = inside ? x : W - 1;
     const uint32_t* row = img + ((size_t)v * P.H + y) * W;
-    const uint32_t p = row[x];
-    uint32_t packed = 0;
-    if (!(P.mask && p == 0)) {
-        const uint32_t up = compute_limit(P, p, y, [&](int k) { return row[x - (ptrdiff_t)k * W]; });
-        const uint32_t dn = compute_limit(P, p, P.H - 1 - y, [&](int k) { return row[x + (ptrdiff_t)k * W]; });
-        const uint32_t lf = compute_limit(P, p, x, [&](int k) { return row[x - k]; });
-        const uint32_t rt = compute_limit(P, p, W - 1 - x, [&](int k) { return row[x + k]; });
-        packed = up | (dn << 8) | (lf << 16) | (rt << 24);
-    }
-    arms[((size_t)v * P.H + y) * W + x] = packed;
+    const uint32_t p = row[xc];
+    const ptrdiff_t step = dir == 0 ? -(ptrdiff_t)W : dir == 1 ? (ptrdiff_t)W : dir == 2 ? -1 : 1;
+    const int avail = dir == 0 ? y : dir == 1 ? P.H - 1 - y : dir == 2 ? xc : W - 1 - xc;
+    uint32_t arm = 0;
+    if (!(P.mask && p == 0)) arm = compute_limit(P, p, avail, [&](int k) { return row[xc + (ptrdiff_t)k * step]; });
+    // gather the quad's four arms into lane dir == 0 (up | down << 8 | left << 16 | right << 24)
+    uint32_t packed = arm << (8 * dir);
+    packed |= (uint32_t)__shfl_xor((int)packed, 1);
+    packed |= (uint32_t)__shfl_xor((int)packed, 2);
+    if (inside && dir == 0) arms[((size_t)v * P.H + y) * W + x] = packed;
 }
 
 __device__ __forceinline__ int arm_up(uint32_t a) { return a & 0xff; }
@@ -888,8 +892,8 @@ int launch_aggregation_pass(float* vol, const uint32_t* arms, const int32_t* ws,
 }
 
 void launch_arms(const uint32_t* img, uint32_t* arms, const DevParams& P, hipStream_t st) {
-    dim3 g((P.W + 127) / 128, P.H, 2 * P.npairs);
-    hipLaunchKernelGGL(k_arms, g, dim3(128), 0, st, img, arms, P); trace_point("k_arms", st);
+    dim3 g((4 * P.W + 255) / 256, P.H, 2 * P.npairs);
+    hipLaunchKernelGGL(k_arms, g, dim3(256), 0, st, img, arms, P); trace_point("k_arms", st);
 }
 
 void launch_window_sizes(const uint32_t* arms, int32_t* ws, const DevParams& P, hipStream_t st) {

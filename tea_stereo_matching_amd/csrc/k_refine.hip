@@ -787,12 +787,13 @@ void launch_region_voting(RefineBufs& B, const uint32_t* arms0, int hf, const De
                        B.out_list, B.dtmp, ps);
     trace_point("k_oscan_scatter", st);
     // grid-stride over the ranked outliers (their count stays on the device)
-    const int vc_blocks = std::max(64, 1536 / std::max(1, P.npairs));
+    // latency-bound walks: single pairs take enough waves to keep every SIMD several deep
+    const int vc_blocks = std::max(64, 4096 / std::max(1, P.npairs));
     hipLaunchKernelGGL(k_vote_count_rank, grid1d(vc_blocks, P), dim3(256), 0, st, B.dm, arms0, B.out_list,
                        B.counts, B.cvote, B.csamp, hf, P);
     trace_point("k_vote_count_rank", st);
     const size_t lds = (size_t)(VD_THREADS / 64) * P.L * sizeof(int);
-    const int vd_blocks = std::max(128, 1024 / std::max(1, P.npairs));
+    const int vd_blocks = std::max(128, 4096 / std::max(1, P.npairs));
     hipLaunchKernelGGL(k_vote_decide_rank, grid1d(vd_blocks, P), dim3(VD_THREADS), lds, st, B.dm, B.dtmp,
                        arms0, B.out_list, B.cvote, B.csamp, B.counts, hf, P);
     trace_point("k_vote_decide_rank", st);
