@@ -271,22 +271,39 @@ __global__ __launch_bounds__(VD_THREADS) void k_vote_decide_rank(
                 if (dv >= minD) atomicAdd(&hist[dv - minD], 1);
             }
         }
-        // carried: ranks r-1, r-2, ... down to (not including) the previous high-vote one
-        for (int top = r - 1; top >= 0; top -= 64) {
-            const int k = top - lane;
-            const int ck = k >= 0 ? cvote[k] : 0;
-            const uint64_t him = __ballot(k >= 0 && ck > thr);
-            const int stop = him ? (int)__builtin_ctzll(him) : 64;  // first high-vote lane (nearest r)
-            if (k >= 0 && lane < stop) {
-                const uint32_t* s = reinterpret_cast<const uint32_t*>(csamp + (size_t)k * kMaxSamples);
-                uint32_t wv[kMaxSamples / 2];
+        // carried: ranks r-1, r-2, ... down to (not including) the previous high-vote one.
+        // Runs of low-vote outliers reach thousands of ranks (config B: up to ~4900 in the
+        // first iteration), so VD_CH chunks of 64 ranks are read per round trip: the votes
+        // of the whole window are in flight at once, the ballots then find the stop.
+        constexpr int VD_CH = 8;
+        for (int top = r - 1; top >= 0; top -= 64 * VD_CH) {
+            int ck[VD_CH];
 #pragma unroll
-                for (int i = 0; i < kMaxSamples / 2; ++i) wv[i] = s[i];
-#pragma unroll
-                for (int m = 0; m < kMaxSamples; ++m)
-                    if (m < ck) atomicAdd(&hist[(wv[m >> 1] >> (16 * (m & 1))) & 0xffffu], 1);
+            for (int u = 0; u < VD_CH; ++u) {
+                const int k = top - 64 * u - lane;
+                ck[u] = k >= 0 ? cvote[k] : 0;
             }
-            if (him) break;
+            int stop_u = VD_CH, stop_l = 64;  // first high-vote rank below r: chunk, lane
+#pragma unroll
+            for (int u = VD_CH - 1; u >= 0; --u) {
+                const uint64_t him = __ballot(top - 64 * u - lane >= 0 && ck[u] > thr);
+                if (him) { stop_u = u; stop_l = (int)__builtin_ctzll(him); }
+            }
+#pragma unroll
+            for (int u = 0; u < VD_CH; ++u) {
+                const int k = top - 64 * u - lane;
+                // low-vote ranks with samples, nearer r than the stop
+                if (u <= stop_u && k >= 0 && (u < stop_u || lane < stop_l) && ck[u] > 0) {
+                    const uint32_t* s = reinterpret_cast<const uint32_t*>(csamp + (size_t)k * kMaxSamples);
+                    uint32_t wv[kMaxSamples / 2];
+#pragma unroll
+                    for (int i = 0; i < kMaxSamples / 2; ++i) wv[i] = s[i];
+#pragma unroll
+                    for (int m = 0; m < kMaxSamples; ++m)
+                        if (m < ck[u]) atomicAdd(&hist[(wv[m >> 1] >> (16 * (m & 1))) & 0xffffu], 1);
+                }
+            }
+            if (stop_u < VD_CH) break;
         }
         __builtin_amdgcn_wave_barrier();
         __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");

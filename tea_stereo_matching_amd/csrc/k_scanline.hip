@@ -287,8 +287,16 @@ __device__ __forceinline__ int omp_start(int t, int n, int T) {
     return t * q + (t < r ? t : r);
 }
 
-template <int J, int SC_K, bool HORIZ, bool MASK, bool WTA, bool OMP>
-__global__ __launch_bounds__(256) void k_scan_line(float* __restrict__ vol,
+// HELP (leftward pass of one or two pairs, J = 1): the argmin leaves the serial chain.
+// A workgroup holds SH_LINES lines, each a chain wave plus a helper wave: the chain wave
+// writes every step's final vector into an LDS ring of two blocks of SC_K steps, and after
+// each block's barrier the helper takes the argmins of the block just finished (under one
+// wave per SIMD the WTA's ballots and readlanes otherwise sit on every step of the chain:
+// 0.57 against 0.30 ms a pass).
+constexpr int SH_LINES = 4;
+
+template <int J, int SC_K, bool HORIZ, bool MASK, bool WTA, bool OMP, bool HELP = false>
+__global__ __launch_bounds__(HELP ? 2 * SH_LINES * 64 : 256) void k_scan_line(float* __restrict__ vol,
                                                    const uint8_t* __restrict__ grad,
                                                    const uint32_t* __restrict__ img, int dir,
                                                    int32_t* __restrict__ wta, int store_view1,
@@ -297,9 +305,15 @@ __global__ __launch_bounds__(256) void k_scan_line(float* __restrict__ vol,
     const DevParams P = Pk;
     const int H = P.H, W = P.W, Lp = P.Lp;
     const int lane = threadIdx.x & 63;
-    const int line = __builtin_amdgcn_readfirstlane(blockIdx.x * 4 + (threadIdx.x >> 6));
+    static_assert(!HELP || (J == 1 && HORIZ && WTA), "the helper form is the single-vector WTA pass");
+    const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    int line = HELP ? (int)blockIdx.x * SH_LINES + wv % SH_LINES : (int)blockIdx.x * 4 + wv;
     pair_shift(blockIdx.z, P.pstride, vol, grad, img, wta);  // infvec: shared, not per pair
     const int v = blockIdx.y;
+    // HELP: every wave of the workgroup takes the same barriers, so a line past the image
+    // re-walks the last line with its stores off instead of leaving
+    const bool dummy = HELP && line >= H;
+    if (dummy) line = H - 1;
     if (line >= (HORIZ ? H : W)) return;
     const ScanConst C = scan_const(P);
     const int len = HORIZ ? W : H;
@@ -314,8 +328,73 @@ __global__ __launch_bounds__(256) void k_scan_line(float* __restrict__ vol,
     const bool rev = sgn < 0;
     const int n = len - 1;
     const int T = OMP ? P.omp_threads : 1;
-    const bool store = !(WTA && v == 1 && !store_view1);
+    const bool store = !(WTA && v == 1 && !store_view1) && !dummy;
     int32_t* wrow = WTA ? wta + ((size_t)v * H + line) * W : nullptr;
+    extern __shared__ __attribute__((aligned(16))) f32x4 sh_ring[];
+    // per line: the vectors of 2 * SC_K steps (1 KB each), then their minima (one dword a lane)
+    char* const hline = reinterpret_cast<char*>(sh_ring) + (size_t)(wv % SH_LINES) * (2 * SC_K * 1280);
+    char* const hring = hline + lane * 16;
+    char* const mring = hline + 2 * SC_K * 1024 + lane * 4;
+    auto barrier = [&]() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); };
+    if constexpr (HELP) if (wv >= SH_LINES) {
+        // helper: after the barrier closing block i, the argmins of block i's steps
+        const int nfull = n / SC_K;
+        const int posbase = dir > 0 ? 1 : len - 2;
+        int dacc = 0;
+        // the block's vectors first (one LDS latency a block), then its argmins: a full
+        // block is branch-free straight-line code, so the 16 steps' chains interleave
+        // the first d holding the step's minimum m (the chain's own): four ballots, the rest
+        // scalar.  m not below FLT_MAX: the reference leaves the disparity unset (minD).
+        // minD > 0 restricts the minimum to [minD, L): the general form.
+        const bool fast = P.minD == 0;
+        auto argmin_of = [&](const f32x4& xk, uint32_t mv) {
+            const f32x4 (&xv)[1] = *reinterpret_cast<const f32x4(*)[1]>(&xk);
+            if (!fast) return vec_argmin_nb<J>(xv, lane, P.L, P.minD, vec_min_bits<J, true>(xv));
+            const uint32_t m = __builtin_amdgcn_readfirstlane(mv);
+            int d = 1 << 20;
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+                const uint64_t b = __ballot(fbits(xk[e]) == m);
+                d = b ? min(d, 4 * (int)__builtin_ctzll(b) + e) : d;
+            }
+            return (bitsf(m) < 3.402823466e+38f && d < (1 << 20)) ? d : 0;
+        };
+        auto flush = [&](int it) {  // the group of 64 steps holding step it, up to it
+            const int g0 = it & ~63;
+            if (!dummy && lane <= it - g0) wrow[posbase + dir * (g0 + lane)] = dacc;
+        };
+        for (int i = 0; i <= nfull; ++i) {
+            barrier();
+            f32x4 x[SC_K];
+            uint32_t mk[SC_K];
+            const char* hb = hring + (i & 1) * (SC_K * 1024);
+            const char* mb = mring + (i & 1) * (SC_K * 256);
+#pragma unroll
+            for (int k = 0; k < SC_K; ++k) {
+                x[k] = *reinterpret_cast<const f32x4*>(hb + k * 1024);
+                mk[k] = *reinterpret_cast<const uint32_t*>(mb + k * 256);
+            }
+            const int i0 = i * SC_K;
+            if (i < nfull) {
+#pragma unroll
+                for (int k = 0; k < SC_K; ++k) {
+                    const int d = argmin_of(x[k], mk[k]);
+                    dacc = lane == ((i0 + k) & 63) ? d : dacc;
+                }
+                if (((i0 + SC_K) & 63) == 0) flush(i0 + SC_K - 1);
+            } else {
+#pragma unroll
+                for (int k = 0; k < SC_K; ++k) {
+                    if (i0 + k < n) {
+                        const int d = argmin_of(x[k], mk[k]);
+                        dacc = lane == ((i0 + k) & 63) ? d : dacc;
+                    }
+                }
+                if ((n & 63) != 0) flush(n - 1);
+            }
+        }
+        return;
+    }
     // byte misalignment of every lane's d2 window (uniform: lanes differ by multiples of 4)
     const int x0a = (HORIZ ? (dir < 0 ? 1 : 0) : line) + C.gpad + sgn * C.minD - (sgn > 0 ? 0 : 3);
     const int posbase = dir > 0 ? 1 : len - 2;  // pos(it) = posbase + dir*it (HORIZ shifts x0)
@@ -340,7 +419,7 @@ __global__ __launch_bounds__(256) void k_scan_line(float* __restrict__ vol,
     uint32_t mq = vec_min_bits<J>(q);
     if (WTA) {
         const int d = vec_argmin<J>(q, lane, C.L, C.minD, mq);
-        if (lane == 0) wrow[p0] = d;
+        if (lane == 0 && !dummy) wrow[p0] = d;
     }
     f32x4 qorig[J];
     uint32_t mqorig = mq;
@@ -430,7 +509,10 @@ __global__ __launch_bounds__(256) void k_scan_line(float* __restrict__ vol,
 #pragma unroll
         for (int j = 0; j < J; ++j) cur[j] += dstep[j];
         mq = vec_min_bits<J, true>(q);
-        if (WTA) {  // step it's index lands in lane it & 63, stored 64 steps at a time
+        if constexpr (HELP) {  // the final vector to the helper's ring (slot it mod 2K)
+            *reinterpret_cast<f32x4*>(hring + (size_t)((it % (2 * SC_K)) * 1024)) = q[0];
+            *reinterpret_cast<uint32_t*>(mring + (size_t)((it % (2 * SC_K)) * 256)) = mq;
+        } else if (WTA) {  // step it's index lands in lane it & 63, stored 64 steps at a time
             const int d = vec_argmin_nb<J>(q, lane, C.L, C.minD, mq);  // whole wave
             dacc = lane == (it & 63) ? d : dacc;
         }
@@ -460,12 +542,43 @@ __global__ __launch_bounds__(256) void k_scan_line(float* __restrict__ vol,
         [&]<int... Ks>(std::integer_sequence<int, Ks...>) {
             (step(IC<Ks>{}, b + Ks), ...);
         }(std::make_integer_sequence<int, SC_K>{});
-        if (WTA && ((b + SC_K) & 63) == 0) flush_wta(b);
+        if constexpr (HELP) barrier();
+        else if (WTA && ((b + SC_K) & 63) == 0) flush_wta(b);
     }
     [&]<int... Ks>(std::integer_sequence<int, Ks...>) {
         ((b + Ks < n ? step(IC<Ks>{}, b + Ks) : (void)0), ...);
     }(std::make_integer_sequence<int, SC_K>{});
-    if (WTA && (n & 63) != 0) flush_wta(n - 1);
+    if constexpr (HELP) barrier();
+    else if (WTA && (n & 63) != 0) flush_wta(n - 1);
+}
+
+// the helper form of the leftward WTA pass (single-vector label axis, K = 16)
+template <bool MASK, bool OMP>
+static void launch_scan_help_t(float* vol, const uint8_t* grad, const uint32_t* img, int dir, int32_t* wta,
+                               int store_view1, const float* infvec, const DevParams& P, hipStream_t st) {
+    constexpr int K = 16;
+    const size_t lds = (size_t)SH_LINES * 2 * K * 1280;
+    static bool attr = false;
+    if (!attr) {
+        (void)hipFuncSetAttribute((const void*)k_scan_line<1, K, true, MASK, true, OMP, true>,
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+        attr = true;
+    }
+    const dim3 g((P.H + SH_LINES - 1) / SH_LINES, 2, P.npairs);
+    hipLaunchKernelGGL((k_scan_line<1, K, true, MASK, true, OMP, true>), g, dim3(2 * SH_LINES * 64), lds, st, vol,
+                       grad, img, dir, wta, store_view1, infvec, P);
+}
+
+static void launch_scan_help(float* vol, const uint8_t* grad, const uint32_t* img, int dir, int32_t* wta,
+                             int store_view1, const float* infvec, const DevParams& P, hipStream_t st) {
+    const bool omp = P.omp_threads > 1;
+    if (P.mask) {
+        if (omp) launch_scan_help_t<true, true>(vol, grad, img, dir, wta, store_view1, infvec, P, st);
+        else launch_scan_help_t<true, false>(vol, grad, img, dir, wta, store_view1, infvec, P, st);
+    } else {
+        if (omp) launch_scan_help_t<false, true>(vol, grad, img, dir, wta, store_view1, infvec, P, st);
+        else launch_scan_help_t<false, false>(vol, grad, img, dir, wta, store_view1, infvec, P, st);
+    }
 }
 
 template <int J, int K, bool HORIZ, bool MASK, bool WTA>
@@ -498,7 +611,8 @@ static int launch_scan(float* vol, const uint8_t* grad, const uint32_t* img, int
     const bool deep = HORIZ && P.npairs <= 2;
     if (J == 1) {
         if constexpr (HORIZ) {
-            if (deep) launch_scan_m<1, 16, HORIZ, WTA>(vol, grad, img, dir, wta, store_view1, infvec, P, st);
+            if (deep && WTA) launch_scan_help(vol, grad, img, dir, wta, store_view1, infvec, P, st);
+            else if (deep) launch_scan_m<1, 16, HORIZ, WTA>(vol, grad, img, dir, wta, store_view1, infvec, P, st);
             else launch_scan_m<1, 8, HORIZ, WTA>(vol, grad, img, dir, wta, store_view1, infvec, P, st);
         } else {
             (void)deep;
