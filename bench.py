@@ -184,6 +184,14 @@ def main():
         for i in range(10):
             m.compute(lh[i % B], rh[i % B])
         host_leg["single_frame_ms"] = round((time.perf_counter() - t1) / 10 * 1e3, 3)
+        # the same frame-at-a-time call on device-resident images (no PCIe in the loop)
+        m.compute_device_ptr(lp[0], rp[0], H, W, W * 3, op[0], W * 4)
+        m.synchronize()
+        t1 = time.perf_counter()
+        for i in range(10):
+            m.compute_device_ptr(lp[i % B], rp[i % B], H, W, W * 3, op[i % B], W * 4)
+            m.synchronize()
+        host_leg["single_frame_device_ms"] = round((time.perf_counter() - t1) / 10 * 1e3, 3)
         m.setConcurrency(args.concurrency)
 
     # Roofline phase (untimed): the same pairs through ONE pipeline, so the cost-volume

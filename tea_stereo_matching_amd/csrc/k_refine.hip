@@ -117,9 +117,7 @@ __global__ void k_scan_blocks(int32_t* __restrict__ bsum, int nb, int32_t* __res
 }
 
 
-// One wave per high-vote outlier: LDS histogram of its own region + carried samples,
-// then the first argmax and the ratio test (:1137-1153).
-constexpr int VD_THREADS = 256;
+constexpr int VD_THREADS = 512;  // the vote decision: threads a high-vote outlier
 
 
 // ---------------------------------------------------------------------------
@@ -150,9 +148,18 @@ __global__ void k_oscan_count(const int32_t* __restrict__ disp, int n, int minD,
 
 // out_list[rank] = pixel of each outlier; dtmp = disp everywhere (the Jacobi output
 // starts as the input; the decision overwrites high-vote outliers)
+// High-vote rank bitmaps (filled by the vote count, read by the decision): level 0 holds one
+// bit per rank, level 1 one bit per level-0 word; a block of SC_BLOCK pixels clears the
+// words its ranks can reach (ranks < pixels).
+constexpr int VB_L0 = SC_BLOCK / 32, VB_L1 = SC_BLOCK / 1024;  // words per scan block
+__host__ __device__ inline size_t vote_bits_words(int nb) { return (size_t)nb * (VB_L0 + VB_L1); }
+
 __global__ void k_oscan_scatter(const int32_t* __restrict__ disp, int n, int minD, const int32_t* __restrict__ bsum,
-                                int32_t* __restrict__ out_list, int32_t* __restrict__ dtmp, size_t ps) {
-    pair_shift(blockIdx.z, ps, disp, bsum, out_list, dtmp);
+                                int32_t* __restrict__ out_list, int32_t* __restrict__ dtmp,
+                                uint32_t* __restrict__ vbits, size_t ps) {
+    pair_shift(blockIdx.z, ps, disp, bsum, out_list, dtmp, vbits);
+    if (threadIdx.x < VB_L0) vbits[blockIdx.x * VB_L0 + threadIdx.x] = 0u;
+    if (threadIdx.x < VB_L1) vbits[(size_t)gridDim.x * VB_L0 + blockIdx.x * VB_L1 + threadIdx.x] = 0u;
     __shared__ int sa[SC_THREADS], sb[SC_THREADS];
     const int base = blockIdx.x * SC_BLOCK + threadIdx.x * SC_ITEMS;
     int a = 0, b = 0;
@@ -179,9 +186,9 @@ __global__ __launch_bounds__(256) void k_vote_count_rank(const int32_t* __restri
                                                          const int32_t* __restrict__ out_list,
                                                          const int32_t* __restrict__ counts,
                                                          int32_t* __restrict__ cvote, uint16_t* __restrict__ csamp,
-                                                         int hf, DevParams Pk) {
+                                                         uint32_t* __restrict__ vbits, int nb, int hf, DevParams Pk) {
     const DevParams P = Pk;
-    pair_shift(blockIdx.z, P.pstride, disp, arms, out_list, counts, cvote, csamp);
+    pair_shift(blockIdx.z, P.pstride, disp, arms, out_list, counts, cvote, csamp, vbits);
     const int lane = threadIdx.x & 63, sub = lane & 15, base = lane & ~15;
     const int W = P.W, minD = P.minD;
     const int nout = counts[0];
@@ -223,101 +230,175 @@ __global__ __launch_bounds__(256) void k_vote_count_rank(const int32_t* __restri
         }
         const int total = __shfl(incl, base + 15);
         if (valid && total <= kMaxSamples && mine > 0) walk(true, incl - mine, csamp + (size_t)a * kMaxSamples);
-        if (valid && sub == 0) cvote[a] = total;
+        if (valid && sub == 0) {
+            cvote[a] = total;
+            if (total > P.voting_thresh) {
+                atomicOr(&vbits[a >> 5], 1u << (a & 31));
+                atomicOr(&vbits[(size_t)nb * VB_L0 + (a >> 10)], 1u << ((a >> 5) & 31));
+            }
+        }
     }
 }
 
-// One wave per high-vote ranked outlier (grid-stride): LDS histogram of its own region,
-// plus the samples of the low-vote outliers ranked between the previous high-vote one
-// and it, then the first argmax and the ratio test (:1137-1153).
+// bits 0..b of a word
+__device__ __forceinline__ uint32_t mask_le(int b) { return b >= 31 ? ~0u : (2u << b) - 1u; }
+
+// The nearest high-vote rank below r (-1: none), from the two-level bitmap: the rank's own
+// word, then 64 summary words (65536 ranks) per read.  Wave-uniform.
+__device__ __forceinline__ int prev_high_rank(const uint32_t* __restrict__ l0, const uint32_t* __restrict__ l1,
+                                              int r, int lane) {
+    const int t = r - 1;
+    if (t < 0) return -1;
+    const int u = t >> 5;
+    const uint32_t wd = l0[u] & mask_le(t & 31);
+    if (wd) return u * 32 + 31 - __builtin_clz(wd);
+    for (int v = u - 1; v >= 0; v = ((v >> 5) - 64) * 32 + 31) {
+        const int s = (v >> 5) - lane;
+        uint32_t sw = s >= 0 ? l1[s] : 0u;
+        if (lane == 0) sw &= mask_le(v & 31);
+        const uint64_t ball = __ballot(sw != 0u);
+        if (ball) {
+            const int ln = (int)__builtin_ctzll(ball);
+            const uint32_t swl = (uint32_t)__builtin_amdgcn_readlane((int)sw, ln);
+            const int u2 = ((v >> 5) - ln) * 32 + 31 - __builtin_clz(swl);
+            const uint32_t w2 = l0[u2];
+            return u2 * 32 + 31 - __builtin_clz(w2);
+        }
+        if ((v >> 5) < 64) break;
+    }
+    return -1;
+}
+
+// The high-vote ranked outliers by quarter words of the bitmap (up to 8 ranks, grid-stride):
+// wave j of the workgroup builds rank r_j's LDS histogram of its own region, the whole
+// workgroup then adds the samples of the low-vote outliers ranked between the previous
+// high-vote one (found in the bitmap) and each r_j -- the histogram the reference carries in
+// raster order (:1132-1151) -- VD_CB ranks a thread per round trip, and wave j takes the first
+// argmax and the ratio test (:1137-1153).
+constexpr int VD_CB = 8;
 __global__ __launch_bounds__(VD_THREADS) void k_vote_decide_rank(
     const int32_t* __restrict__ disp, int32_t* __restrict__ dtmp, const uint32_t* __restrict__ arms,
     const int32_t* __restrict__ out_list, const int32_t* __restrict__ cvote, const uint16_t* __restrict__ csamp,
-    const int32_t* __restrict__ counts, int hf, DevParams Pk) {
+    const int32_t* __restrict__ counts, const uint32_t* __restrict__ vbits, int nb, int hf, DevParams Pk) {
     const DevParams P = Pk;
-    pair_shift(blockIdx.z, P.pstride, disp, dtmp, arms, out_list, cvote, csamp, counts);
-    extern __shared__ int hist_all[];
-    const int L = P.L, W = P.W, minD = P.minD, thr = P.voting_thresh;
-    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    int* hist = hist_all + wave * L;
+    pair_shift(blockIdx.z, P.pstride, disp, dtmp, arms, out_list, cvote, csamp, counts, vbits);
+    extern __shared__ int hist[];
+    const int L = P.L, W = P.W, minD = P.minD;
+    const int tid = threadIdx.x, lane = tid & 63;
+    const uint32_t* l0 = vbits;
+    const uint32_t* l1 = vbits + (size_t)nb * VB_L0;
     const int nout = counts[0];
-    const int nwaves = gridDim.x * (VD_THREADS / 64);
-    for (int r = blockIdx.x * (VD_THREADS / 64) + wave; r < nout; r += nwaves) {
-        const int v = cvote[r];
-        if (v <= thr) continue;  // low vote: the pixel keeps its value (dtmp holds it)
-        for (int d = lane; d < L; d += 64) hist[d] = 0;
-        __builtin_amdgcn_wave_barrier();
-        const int p = out_list[r];
-        const int y = p / W, x = p - y * W;
-        int oA, oB, iA, iB;
-        region_arms(arms[p], hf, oA, oB, iA, iB);
-        for (int o = -oA + lane; o <= oB; o += 64) {
-            const int yy0 = hf ? y + o : y, xx0 = hf ? x : x + o;
-            int a1, b1, a2, b2;
-            region_arms(arms[(size_t)yy0 * W + xx0], hf, a1, b1, a2, b2);
-            const ptrdiff_t st = hf ? 1 : W;
-            const int32_t* rp = disp + (size_t)yy0 * W + xx0;
-            int i = -a2;
-            for (; i + 3 <= b2; i += 4) {
-                const int d0 = rp[(ptrdiff_t)i * st], d1 = rp[(ptrdiff_t)(i + 1) * st];
-                const int d2 = rp[(ptrdiff_t)(i + 2) * st], d3 = rp[(ptrdiff_t)(i + 3) * st];
-                if (d0 >= minD) atomicAdd(&hist[d0 - minD], 1);
-                if (d1 >= minD) atomicAdd(&hist[d1 - minD], 1);
-                if (d2 >= minD) atomicAdd(&hist[d2 - minD], 1);
-                if (d3 >= minD) atomicAdd(&hist[d3 - minD], 1);
-            }
-            for (; i <= b2; ++i) {
-                const int dv = rp[(ptrdiff_t)i * st];
-                if (dv >= minD) atomicAdd(&hist[dv - minD], 1);
+    const int nwords = (nout + 31) >> 5;
+    // workgroup b takes bits [8q, 8q + 8) (q = b mod 4) of the words b / 4 + k G4: clustered
+    // high-vote outliers (tens to a word) are spread over four workgroups.  Its words are
+    // read in one round trip (a thread each) and the non-empty ones listed in LDS.
+    __shared__ uint32_t s_list[VD_THREADS][2];
+    __shared__ int s_n;
+    const int q = blockIdx.x & 3, G4 = gridDim.x >> 2, w0 = blockIdx.x >> 2;
+    const int nk = w0 < nwords ? (nwords - w0 + G4 - 1) / G4 : 0;
+    for (int kb = 0; kb < nk; kb += VD_THREADS) {
+        if (tid == 0) s_n = 0;
+        __syncthreads();
+        if (kb + tid < nk) {
+            const int wi = w0 + (kb + tid) * G4;
+            const uint32_t wd = l0[wi] & (0xffu << (8 * q));
+            if (wd) {
+                const int slot = atomicAdd(&s_n, 1);
+                s_list[slot][0] = (uint32_t)wi;
+                s_list[slot][1] = wd;
             }
         }
-        // carried: ranks r-1, r-2, ... down to (not including) the previous high-vote one.
-        // Runs of low-vote outliers reach thousands of ranks (config B: up to ~4900 in the
-        // first iteration), so VD_CH chunks of 64 ranks are read per round trip: the votes
-        // of the whole window are in flight at once, the ballots then find the stop.
-        constexpr int VD_CH = 8;
-        for (int top = r - 1; top >= 0; top -= 64 * VD_CH) {
-            int ck[VD_CH];
+        __syncthreads();
+        const int nl = s_n;
+        for (int li = 0; li < nl; ++li) {
+            // the quarter word's high-vote ranks r_0 < ... < r_{nr-1}: no other high-vote rank
+            // lies between them, so r_j's carry is (r_{j-1}, r_j) and r_0's is (prev, r_0)
+            const int wi = (int)s_list[li][0];
+            const uint32_t word = s_list[li][1];
+            const int nr = __builtin_popcount(word);
+            for (int d = tid; d < nr * L; d += VD_THREADS) hist[d] = 0;
+            int rk[8];
+            {
+                uint32_t wb = word;
 #pragma unroll
-            for (int u = 0; u < VD_CH; ++u) {
-                const int k = top - 64 * u - lane;
-                ck[u] = k >= 0 ? cvote[k] : 0;
-            }
-            int stop_u = VD_CH, stop_l = 64;  // first high-vote rank below r: chunk, lane
-#pragma unroll
-            for (int u = VD_CH - 1; u >= 0; --u) {
-                const uint64_t him = __ballot(top - 64 * u - lane >= 0 && ck[u] > thr);
-                if (him) { stop_u = u; stop_l = (int)__builtin_ctzll(him); }
-            }
-#pragma unroll
-            for (int u = 0; u < VD_CH; ++u) {
-                const int k = top - 64 * u - lane;
-                // low-vote ranks with samples, nearer r than the stop
-                if (u <= stop_u && k >= 0 && (u < stop_u || lane < stop_l) && ck[u] > 0) {
-                    const uint32_t* s = reinterpret_cast<const uint32_t*>(csamp + (size_t)k * kMaxSamples);
-                    uint32_t wv[kMaxSamples / 2];
-#pragma unroll
-                    for (int i = 0; i < kMaxSamples / 2; ++i) wv[i] = s[i];
-#pragma unroll
-                    for (int m = 0; m < kMaxSamples; ++m)
-                        if (m < ck[u]) atomicAdd(&hist[(wv[m >> 1] >> (16 * (m & 1))) & 0xffffu], 1);
+                for (int j = 0; j < 8; ++j) {
+                    rk[j] = wb ? wi * 32 + (int)__builtin_ctz(wb) : 0x7fffffff;
+                    wb &= wb - 1u;
                 }
             }
-            if (stop_u < VD_CH) break;
+            __syncthreads();
+            // wave j: the own region of r_j into histogram j
+            const int wv = tid >> 6;
+            int p = 0, v = 0;
+            if (wv < nr) {
+                int r = rk[0];
+#pragma unroll
+                for (int j = 1; j < 8; ++j) r = wv == j ? rk[j] : r;
+                v = cvote[r];
+                p = out_list[r];
+                const int y = p / W, x = p - y * W;
+                int oA, oB, iA, iB;
+                region_arms(arms[p], hf, oA, oB, iA, iB);
+                int* h = hist + wv * L;
+                for (int o = -oA + lane; o <= oB; o += 64) {
+                    const int yy0 = hf ? y + o : y, xx0 = hf ? x : x + o;
+                    int a1, b1, a2, b2;
+                    region_arms(arms[(size_t)yy0 * W + xx0], hf, a1, b1, a2, b2);
+                    const ptrdiff_t st = hf ? 1 : W;
+                    const int32_t* rp = disp + (size_t)yy0 * W + xx0;
+                    for (int i = -a2; i <= b2; ++i) {
+                        const int dv = rp[(ptrdiff_t)i * st];
+                        if (dv >= minD) atomicAdd(&h[dv - minD], 1);
+                    }
+                }
+            }
+            // carried: the low-vote ranks with samples in (prev, r_last), each into the
+            // histogram of the first r_j above it, VD_CB ranks a thread per round trip
+            const int lo = prev_high_rank(l0, l1, rk[0], lane) + 1;
+            int rlast = rk[0];
+#pragma unroll
+            for (int j = 1; j < 8; ++j) rlast = j < nr ? rk[j] : rlast;
+            for (int base = lo; base < rlast; base += VD_CB * VD_THREADS) {
+                int ck[VD_CB];
+#pragma unroll
+                for (int c = 0; c < VD_CB; ++c) {
+                    const int k = base + c * VD_THREADS + tid;
+                    ck[c] = k < rlast ? cvote[k] : 0;
+                }
+#pragma unroll
+                for (int c = 0; c < VD_CB; ++c) {
+                    if (ck[c] > 0 && ck[c] <= P.voting_thresh) {
+                        const int k = base + c * VD_THREADS + tid;
+                        int j = 0;
+#pragma unroll
+                        for (int t = 0; t < 7; ++t) j += k > rk[t] ? 1 : 0;
+                        int* h = hist + j * L;
+                        const uint32_t* s = reinterpret_cast<const uint32_t*>(csamp + (size_t)k * kMaxSamples);
+                        uint32_t wv2[kMaxSamples / 2];
+#pragma unroll
+                        for (int i = 0; i < kMaxSamples / 2; ++i) wv2[i] = s[i];
+#pragma unroll
+                        for (int m = 0; m < kMaxSamples; ++m)
+                            if (m < ck[c]) atomicAdd(&h[(wv2[m >> 1] >> (16 * (m & 1))) & 0xffffu], 1);
+                    }
+                }
+            }
+            __syncthreads();
+            if (wv < nr) {  // wave j: first argmax of histogram j, the ratio test
+                const int* h = hist + wv * L;
+                uint64_t best = ~0ull;
+                for (int d = lane; d < L; d += 64) {
+                    const uint64_t key = ((uint64_t)(0xffffffffu - (uint32_t)h[d]) << 32) | (uint32_t)d;
+                    best = key < best ? key : best;
+                }
+                best = wave_min_u64(best);
+                const int cmax = (int)(0xffffffffu - (uint32_t)(best >> 32));
+                const int dbest = (int)(uint32_t)best;
+                const float ratio = cmax / (float)v;
+                if (lane == 0) dtmp[p] = ratio > P.voting_ratio && cmax > 0 ? dbest + minD : disp[p];
+            }
+            __syncthreads();
         }
-        __builtin_amdgcn_wave_barrier();
-        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-        uint64_t best = ~0ull;
-        for (int d = lane; d < L; d += 64) {
-            const uint64_t key = ((uint64_t)(0xffffffffu - (uint32_t)hist[d]) << 32) | (uint32_t)d;
-            best = key < best ? key : best;
-        }
-        best = wave_min_u64(best);
-        const int cmax = (int)(0xffffffffu - (uint32_t)(best >> 32));
-        const int dbest = (int)(uint32_t)best;
-        const float ratio = cmax / (float)v;
-        if (lane == 0) dtmp[p] = ratio > P.voting_ratio && cmax > 0 ? dbest + minD : disp[p];
-        __builtin_amdgcn_wave_barrier();
     }
 }
 
@@ -780,6 +861,7 @@ __global__ void k_arms_to_ref(const uint32_t* __restrict__ arms, int32_t* __rest
 // launchers
 // ---------------------------------------------------------------------------
 size_t refine_scan_blocks(int n) { return (size_t)(n + SC_BLOCK - 1) / SC_BLOCK; }
+size_t refine_vote_bits_bytes(int n) { return vote_bits_words((int)refine_scan_blocks(n)) * 4; }
 
 // every refinement launch covers the group's P.npairs pairs (blockIdx.z = pair)
 static dim3 grid2d(int W, int H, int bx, const DevParams& P) { return dim3((W + bx - 1) / bx, H, P.npairs); }
@@ -801,18 +883,20 @@ void launch_region_voting(RefineBufs& B, const uint32_t* arms0, int hf, const De
     hipLaunchKernelGGL(k_scan_blocks, grid1d(1, P), dim3(SC_THREADS), 0, st, B.bsum, nb, B.counts, ps);
     trace_point("k_scan_blocks", st);
     hipLaunchKernelGGL(k_oscan_scatter, grid1d(nb, P), dim3(SC_THREADS), 0, st, B.dm, n, P.minD, B.bsum,
-                       B.out_list, B.dtmp, ps);
+                       B.out_list, B.dtmp, B.vbits, ps);
     trace_point("k_oscan_scatter", st);
     // grid-stride over the ranked outliers (their count stays on the device)
     // latency-bound walks: single pairs take enough waves to keep every SIMD several deep
     const int vc_blocks = std::max(64, 4096 / std::max(1, P.npairs));
     hipLaunchKernelGGL(k_vote_count_rank, grid1d(vc_blocks, P), dim3(256), 0, st, B.dm, arms0, B.out_list,
-                       B.counts, B.cvote, B.csamp, hf, P);
+                       B.counts, B.cvote, B.csamp, B.vbits, nb, hf, P);
     trace_point("k_vote_count_rank", st);
-    const size_t lds = (size_t)(VD_THREADS / 64) * P.L * sizeof(int);
-    const int vd_blocks = std::max(128, 4096 / std::max(1, P.npairs));
+    // grid-stride over quarter words of the bitmap, one round of resident workgroups (a
+    // workgroup per quarter word of a full image's ranks measured 32 us a launch, most idle)
+    const size_t lds = (size_t)8 * P.L * sizeof(int);  // a histogram per rank of a quarter word
+    const int vd_blocks = 4 * std::max(16, 256 / std::max(1, P.npairs));
     hipLaunchKernelGGL(k_vote_decide_rank, grid1d(vd_blocks, P), dim3(VD_THREADS), lds, st, B.dm, B.dtmp,
-                       arms0, B.out_list, B.cvote, B.csamp, B.counts, hf, P);
+                       arms0, B.out_list, B.cvote, B.csamp, B.counts, B.vbits, nb, hf, P);
     trace_point("k_vote_decide_rank", st);
     std::swap(B.dm, B.dtmp);
 }

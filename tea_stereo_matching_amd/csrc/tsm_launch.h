@@ -58,6 +58,7 @@ struct RefineBufs {
     int32_t* cvote;   // [H][W] vote count by outlier rank (out_pos order)
     uint16_t* csamp;  // [H][W][20] low-vote samples by outlier rank
     int32_t* bsum;    // scan block sums [2 * nblocks]
+    uint32_t* vbits;  // high-vote rank bitmaps: nblocks * (128 level-0 + 4 level-1 words)
     int32_t* counts;  // [4]
     uint8_t* gray;    // [H][W]
     int32_t* hist;    // [256] + 64 ints of LUT scratch
@@ -73,6 +74,7 @@ struct RefineBufs {
     float* subpix;    // [H][W]
 };
 size_t refine_scan_blocks(int n);
+size_t refine_vote_bits_bytes(int n);
 void launch_outlier(RefineBufs& B, const DevParams& P, hipStream_t st);
 void launch_region_voting(RefineBufs& B, const uint32_t* arms0, int horizontal_first,
                           const DevParams& P, hipStream_t st);
