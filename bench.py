@@ -135,14 +135,33 @@ def main():
     if rank == 0 and world > 1 and not args.no_gather:
         gathered = [torch.empty_like(outs) for _ in range(world)]
 
+    # N > 1: each step's gather to rank 0 runs on RCCL's stream while the next step matches:
+    # step k writes output buffer k % 2, and waits (before matching) for the gather that
+    # read that buffer two steps back; the timed region ends after the last gather.
+    gather_on = world > 1 and not args.no_gather
+    outs_b = [outs, torch.empty_like(outs)] if gather_on else [outs]
+    op_b = [[o[i].data_ptr() for i in range(B)] for o in outs_b]
+    works = []
+    nstep = [0]
+
+    def drain():
+        while works:
+            works.pop(0).wait()
+        torch.cuda.synchronize()
+
     def step():
-        m.compute_batch_device_ptr(lp, rp, H, W, W * 3, op, W * 4)
-        if world > 1 and not args.no_gather:
-            Dd.gather_to_root(outs, rank, world, gathered)
+        buf = nstep[0] % len(outs_b)
+        nstep[0] += 1
+        if gather_on and len(works) >= 2:
+            works.pop(0).wait()
+            torch.cuda.current_stream().synchronize()
+        m.compute_batch_device_ptr(lp, rp, H, W, W * 3, op_b[buf], W * 4)
+        if gather_on:
+            works.append(dist.gather(outs_b[buf], gathered if rank == 0 else None, dst=0, async_op=True))
 
     for _ in range(args.warmup):
         step()
-    torch.cuda.synchronize()
+    drain()
     m.setProfiling(True)
     m.resetStageTimes()
     if world > 1:
@@ -151,6 +170,7 @@ def main():
     t0 = time.perf_counter()
     for _ in range(args.steps):
         step()
+    drain()
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
