@@ -20,7 +20,17 @@ static std::string thrown_string(F f) {
     return "<none>";
 }
 
-int main() {
+// argv[1] (optional): a directory where the pair and its disparity are written (raw
+// left/right BGR bytes, fp32 disparity) for the Python driver to compare with the oracle
+static void dump(const char* dir, const char* name, const void* p, size_t n) {
+    const std::string path = std::string(dir) + "/" + name;
+    FILE* f = std::fopen(path.c_str(), "wb");
+    if (!f) { std::printf("FAIL cannot write %s\n", path.c_str()); ++fails; return; }
+    if (std::fwrite(p, 1, n, f) != n) { std::printf("FAIL short write %s\n", path.c_str()); ++fails; }
+    std::fclose(f);
+}
+
+int main(int argc, char** argv) {
     const int H = 48, W = 80;
     std::vector<unsigned char> l(H * W * 3), r(H * W * 3);
     unsigned s = 12345;
@@ -45,6 +55,11 @@ int main() {
     for (float v : d.data) { if (v >= 0) { ++valid; if (v > 5.5f && v < 6.5f) ++six; } }
     CHECK(valid > H * W / 2);
     CHECK(six > valid * 8 / 10);
+    if (argc > 1) {
+        dump(argv[1], "left.bgr", l.data(), l.size());
+        dump(argv[1], "right.bgr", r.data(), r.size());
+        dump(argv[1], "disp.f32", d.data.data(), d.data.size() * sizeof(float));
+    }
 
     CHECK(thrown_string([&] { adcensus.setMinMaxDisparity(-3, 3); }) == "[ADCensus] Set MinMaxDisparity error.");
     CHECK(thrown_string([&] { adcensus.setMinMaxDisparity(9, 9); }) == "[ADCensus] Set MinMaxDisparity error.");

@@ -1,10 +1,12 @@
-"""Compile and run the C++ API check (tests/cpp/test_stereo_api.cpp) on the GPU box."""
+"""Compile and run the C++ API check (tests/cpp/test_stereo_api.cpp) on the GPU box; its
+disparity is then compared with the oracle's, bit for bit."""
 import os
 import subprocess
 
+import numpy as np
 import pytest
 
-from conftest import ROOT
+from conftest import ROOT, host_threads
 
 pytestmark = pytest.mark.gpu
 
@@ -16,6 +18,15 @@ def test_cpp_stereo_api(tmp_path):
                     os.path.join(ROOT, "tests", "cpp", "test_stereo_api.cpp"), "-o", exe,
                     f"-L{lib}", "-ltsm_adcensus", f"-Wl,-rpath,{lib}", "-L/opt/rocm/lib",
                     "-lamdhip64", "-Wl,-rpath,/opt/rocm/lib"], check=True)
-    r = subprocess.run([exe], capture_output=True, text=True, timeout=120)
+    r = subprocess.run([exe, str(tmp_path)], capture_output=True, text=True, timeout=120)
     assert r.returncode == 0, r.stdout + r.stderr
     assert "OK" in r.stdout
+    # the C++ class's disparity of its own 48x80 pair, bit-exact against the oracle
+    # (RGB, D = [0, 16], serial scanline: the class's settings in the program)
+    from oracle import oracle as O
+    H, W = 48, 80
+    left = np.fromfile(tmp_path / "left.bgr", np.uint8).reshape(H, W, 3)
+    right = np.fromfile(tmp_path / "right.bgr", np.uint8).reshape(H, W, 3)
+    got = np.fromfile(tmp_path / "disp.f32", np.float32).reshape(H, W)
+    want, _ = O.compute(left, right, O.default_params(O.RGB, 0, 16, num_threads=host_threads()))
+    assert np.array_equal(got, want)
