@@ -292,6 +292,17 @@ def main():
         "unit": "GB/s",
         "frac": round(b_pipe * value / world / 1e9 / HBM_PEAK_GBS, 4),
     }
+    # the volume stages against the same roof, from the roofline phase's per-pair stage
+    # times (one pipeline alone): algorithmic transfers of the two-view volume 2*L*N*4 B --
+    # aggregation 5 launches x (R + W) = 10, scanline 4 x (R + W) - view 1's last write = 7.5
+    vbytes = 2 * L * N * 4
+    line["stage_roofline"] = {}
+    for name, transfers in (("aggregate", 10.0), ("scanline", 7.5)):
+        ms_pair = stage_ms.get(name, 0.0)
+        if ms_pair > 0:
+            gbs = transfers * vbytes / (ms_pair * 1e-3) / 1e9
+            line["stage_roofline"][name] = {"transfers": transfers, "ms_per_pair": ms_pair,
+                                            "achieved": round(gbs, 1), "frac": round(gbs / HBM_PEAK_GBS, 4)}
     if rank == 0:
         line["host_buffers"] = host_leg
         line["hbm_calibration"] = hbm_calibration(L * N * 2 * 4)
