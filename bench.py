@@ -106,9 +106,17 @@ def main():
     from tea_stereo_matching_amd import distributed as Dd
 
     rank, world, local = Dd.world_info()
+    # one GPU per rank; more ranks than GPUs (a one-GPU rehearsal) share them round-robin
+    local = local % max(1, torch.cuda.device_count())
     if world > 1:
         torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        # RCCL over xGMI; TSM_BENCH_BACKEND=gloo rehearses several ranks on one GPU (no
+        # duplicate-GPU communicator), with --no-gather (gloo gathers host tensors only)
+        backend = os.environ.get("TSM_BENCH_BACKEND", "nccl")
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:
+            dist.init_process_group(backend)
     dev = torch.device("cuda", local)
     torch.cuda.set_device(dev)
 
@@ -179,6 +187,17 @@ def main():
     stages_conc = m.stageTimes()
     elapsed = Dd.max_over_ranks(elapsed, world, dev)
     verify = verify_outputs(m, tsm, outs, lefts, rights, seeds, H, W, D)
+    if gather_on:  # rank 0 holds every rank's last-step maps, byte for byte
+        import hashlib
+
+        last = outs_b[(nstep[0] - 1) % len(outs_b)]
+        digests = [None] * world
+        dist.all_gather_object(digests, hashlib.sha256(last.cpu().numpy().tobytes()).hexdigest())
+        if rank == 0:
+            same = all(hashlib.sha256(gathered[r].cpu().numpy().tobytes()).hexdigest() == digests[r]
+                       for r in range(world))
+            verify["ok"] = verify["ok"] and same
+        verify["how"] += "; rank 0's gathered maps == every rank's (SHA-256)"
     verified = Dd.min_over_ranks(1.0 if verify["ok"] else 0.0, world, dev) == 1.0
 
     # Host-buffer leg (untimed for `value`): the same batch handed over as host (pageable
