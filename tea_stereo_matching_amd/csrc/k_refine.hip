@@ -70,8 +70,8 @@ __device__ __forceinline__ void region_arms(uint32_t a, bool hf, int& oA, int& o
     else { oA = lf; oB = rt; iA = up; iB = dn; }
 }
 
-// Device-wide exclusive scan of (outliers, high-vote outliers) per block of SC_BLOCK
-// pixels in raster order (k_oscan_count -> k_scan_blocks -> k_oscan_scatter).
+// Raster-order ranks of the outliers per block of SC_BLOCK pixels (k_oscan_count, then
+// k_oscan_scatter with the preceding blocks' counts).
 constexpr int SC_THREADS = 256, SC_ITEMS = 16, SC_BLOCK = SC_THREADS * SC_ITEMS;
 
 __device__ __forceinline__ void block_scan2(int& a, int& b, int* sa, int* sb) {
@@ -91,29 +91,6 @@ __device__ __forceinline__ void block_scan2(int& a, int& b, int* sa, int* sb) {
     const int ia = sa[t], ib = sb[t];
     a = ia - a;
     b = ib - b;
-}
-
-
-__global__ void k_scan_blocks(int32_t* __restrict__ bsum, int nb, int32_t* __restrict__ counts, size_t ps) {
-    pair_shift(blockIdx.z, ps, bsum, counts);
-    // single block: exclusive scan of nb block totals (nb <= 1024 * 8)
-    __shared__ int sa[SC_THREADS], sb[SC_THREADS];
-    const int per = (nb + SC_THREADS - 1) / SC_THREADS;
-    const int b0 = threadIdx.x * per;
-    int a = 0, b = 0;
-    for (int k = 0; k < per; ++k)
-        if (b0 + k < nb) { a += bsum[2 * (b0 + k)]; b += bsum[2 * (b0 + k) + 1]; }
-    block_scan2(a, b, sa, sb);
-    for (int k = 0; k < per; ++k) {
-        if (b0 + k < nb) {
-            const int ta = bsum[2 * (b0 + k)], tb = bsum[2 * (b0 + k) + 1];
-            bsum[2 * (b0 + k)] = a;
-            bsum[2 * (b0 + k) + 1] = b;
-            a += ta;
-            b += tb;
-        }
-    }
-    if (threadIdx.x == SC_THREADS - 1) { counts[0] = sa[SC_THREADS - 1]; counts[1] = sb[SC_THREADS - 1]; }
 }
 
 
@@ -154,10 +131,21 @@ __global__ void k_oscan_count(const int32_t* __restrict__ disp, int n, int minD,
 constexpr int VB_L0 = SC_BLOCK / 32, VB_L1 = SC_BLOCK / 1024;  // words per scan block
 __host__ __device__ inline size_t vote_bits_words(int nb) { return (size_t)nb * (VB_L0 + VB_L1); }
 
+// Each block's first rank is the sum of the outlier counts of the blocks before it (read
+// and reduced here: a few hundred counts, no separate scan launch); the last block writes
+// the total.
 __global__ void k_oscan_scatter(const int32_t* __restrict__ disp, int n, int minD, const int32_t* __restrict__ bsum,
                                 int32_t* __restrict__ out_list, int32_t* __restrict__ dtmp,
-                                uint32_t* __restrict__ vbits, size_t ps) {
-    pair_shift(blockIdx.z, ps, disp, bsum, out_list, dtmp, vbits);
+                                uint32_t* __restrict__ vbits, int32_t* __restrict__ counts, size_t ps) {
+    pair_shift(blockIdx.z, ps, disp, bsum, out_list, dtmp, vbits, counts);
+    __shared__ int s_base;
+    if (threadIdx.x == 0) s_base = 0;
+    __syncthreads();
+    {
+        int part = 0;
+        for (int i = threadIdx.x; i < (int)blockIdx.x; i += SC_THREADS) part += bsum[2 * i];
+        if (part) atomicAdd(&s_base, part);
+    }
     if (threadIdx.x < VB_L0) vbits[blockIdx.x * VB_L0 + threadIdx.x] = 0u;
     if (threadIdx.x < VB_L1) vbits[(size_t)gridDim.x * VB_L0 + blockIdx.x * VB_L1 + threadIdx.x] = 0u;
     __shared__ int sa[SC_THREADS], sb[SC_THREADS];
@@ -167,8 +155,13 @@ __global__ void k_oscan_scatter(const int32_t* __restrict__ disp, int n, int min
         const int p = base + k;
         if (p < n && disp[p] < minD) a++;
     }
-    block_scan2(a, b, sa, sb);
-    a += bsum[2 * blockIdx.x];
+    block_scan2(a, b, sa, sb);  // its barriers also publish s_base
+    const int first = s_base;
+    a += first;
+    if (threadIdx.x == SC_THREADS - 1 && blockIdx.x == gridDim.x - 1) {
+        counts[0] = first + sa[SC_THREADS - 1];
+        counts[1] = 0;
+    }
     for (int k = 0; k < SC_ITEMS; ++k) {
         const int p = base + k;
         if (p >= n) break;
@@ -880,10 +873,8 @@ void launch_region_voting(RefineBufs& B, const uint32_t* arms0, int hf, const De
     const size_t ps = P.pstride;
     hipLaunchKernelGGL(k_oscan_count, grid1d(nb, P), dim3(SC_THREADS), 0, st, B.dm, n, P.minD, B.bsum, ps);
     trace_point("k_oscan_count", st);
-    hipLaunchKernelGGL(k_scan_blocks, grid1d(1, P), dim3(SC_THREADS), 0, st, B.bsum, nb, B.counts, ps);
-    trace_point("k_scan_blocks", st);
     hipLaunchKernelGGL(k_oscan_scatter, grid1d(nb, P), dim3(SC_THREADS), 0, st, B.dm, n, P.minD, B.bsum,
-                       B.out_list, B.dtmp, B.vbits, ps);
+                       B.out_list, B.dtmp, B.vbits, B.counts, ps);
     trace_point("k_oscan_scatter", st);
     // grid-stride over the ranked outliers (their count stays on the device)
     // latency-bound walks: single pairs take enough waves to keep every SIMD several deep
