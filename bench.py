@@ -53,23 +53,44 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-ops", action="store_true", help="skip the f2-f4 operator leg")
     ap.add_argument("--cpu-threads", type=int, default=0)
+    ap.add_argument("--no-configs", action="store_true",
+                    help="skip the configs block (C, E, B in HSI, B with the T=20 emulation)")
     return ap.parse_args()
+
+
+def host_cpus():
+    """CPUs this process may use: its affinity set, and the cgroup CPU quota when one caps
+    it below that (a GPU box's share).  Returns (threads to use, description)."""
+    aff = len(os.sched_getaffinity(0))
+    quota = None
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            q, period = f.read().split()[:2]
+            if q != "max":
+                quota = max(1, int(int(q) / int(period)))
+    except (OSError, ValueError):
+        pass
+    n = min(aff, quota) if quota else aff
+    desc = f"{aff} CPUs in the process's affinity set" + (f", cgroup quota {quota} CPUs" if quota else ", no cgroup CPU quota")
+    return n, desc
 
 
 def cpu_baseline(args, left, right):
     """Oracle (`port` of the reference path, same per-(p,d) census and OpenMP
-    decomposition) on one pair on this host: ~10-30 s of CPU work."""
+    decomposition) on one pair on this host, on every CPU the process may use
+    (affinity set, capped by a cgroup quota): ~10-30 s of CPU work."""
     from oracle import oracle as O
 
-    threads = args.cpu_threads or min(16, os.cpu_count() or 1)
+    avail, desc = host_cpus()
+    threads = args.cpu_threads or avail
     p = O.default_params(O.RGB, 0, args.max_disparity, num_threads=threads)
     t0 = time.perf_counter()
     O.compute(left, right, p)
     dt = time.perf_counter() - t0
     return {"value": 1.0 / dt, "unit": "pairs/s", "cores": threads, "kind": "port",
             "sample": f"1 synthetic pair (seed 1000) {args.width}x{args.height} D=[0,{args.max_disparity}] "
-                      f"RGB, oracle/ C restatement with OpenMP, {dt:.2f} s/pair",
-            "host_cpus": os.cpu_count(), "cpu_model": cpu_model()}
+                      f"RGB, oracle/ C restatement with OpenMP on {threads} threads, {dt:.2f} s/pair",
+            "host_cpus": os.cpu_count(), "usable_cpus": desc, "cpu_model": cpu_model()}
 
 
 def cpu_model():
@@ -327,17 +348,121 @@ def main():
         line["hbm_calibration"] = hbm_calibration(L * N * 2 * 4)
     if rank == 0 and not args.no_ops:
         line["next_rows"] = ops_leg(tsm, outs, lefts, H, W)
+    m.close()
+    if rank == 0 and world == 1 and not args.no_configs and (H, W, D) == (375, 1242, 192):
+        del outs, outs_b
+        torch.cuda.empty_cache()
+        line["configs"] = configs_leg(tsm, dev, lefts, rights)
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         l, r, _ = tsm.synthetic.make_scene(1000, H, W, L)
         line["cpu_baseline"] = cpu_baseline(args, l, r)
         line["speedup_vs_cpu_baseline"] = round(value / line["cpu_baseline"]["value"], 1)
     else:
         line["cpu_baseline"] = None
-    m.close()
+    from tea_stereo_matching_amd import _native as Nn
+    line["library"] = os.path.relpath(Nn.LOADED_PATH, ROOT) if Nn.LOADED_PATH else None
     if rank == 0:
         print(json.dumps(line), flush=True)
     if world > 1:
         dist.destroy_process_group()
+
+
+# The configs block: BASELINE.json's other single-GPU configs and the modes beside the
+# headline (untimed for `value`).  (name, workload, H, W, D, colour model, omp threads,
+# grey, first seed, pairs, pairs per group, golden-hash key of the first pair)
+CONFIGS = [
+    ("C", "config C: 1500x1000 BGR, setMinMaxDisparity(0,256), RGB", 1000, 1500, 256, 0, 0, False, 2000, 16, 8, "C"),
+    ("E", "config E: 2048x1536 grey -> BGR, setMinMaxDisparity(0,320), RGB", 1536, 2048, 320, 0, 0, True, 3000, 8, 4, "E"),
+    ("B_HSI", "config B in the reference's default HSI model", 375, 1242, 192, 1, 0, False, 1000, 128, 64, "B_HSI_1000"),
+    ("B_OMP20", "config B, RGB, setOmpEmulation(20): equals the reference's shipped outputs", 375, 1242, 192, 0, 20,
+     False, 1000, 128, 64, "B_OMP20_1000"),
+]
+
+
+def configs_leg(tsm, dev, b_lefts, b_rights, reps=2):
+    """Per config: pairs/s and ms/frame of the device batch entry (inputs in HBM, groups of
+    `K` pairs over the two group streams, `reps` batches after one warm-up, wall clock
+    around synchronised batches), one frame's device-resident latency, the cost walk's
+    launch time alone (HIP events, groups of one) against B_build, and pair 0's SHA-256
+    against the oracle's (tests/golden/config_hashes.json)."""
+    import hashlib
+
+    import numpy as np
+    import torch
+
+    try:
+        with open(os.path.join(ROOT, "tests", "golden", "config_hashes.json")) as f:
+            gold = json.load(f)
+    except OSError:
+        gold = {}
+    res = {}
+    for name, desc, H, W, D, model, omp, grey, seed0, n, K, key in CONFIGS:
+        L = D + 1
+        if (H, W) == (375, 1242) and seed0 == 1000:
+            lefts, rights = b_lefts[:n], b_rights[:n]
+        else:
+            lefts, rights = [], []
+            for l, r, _ in tsm.synthetic.make_scene_batch(range(seed0, seed0 + n), H, W, L,
+                                                          threads=min(16, os.cpu_count() or 1), grayscale=grey):
+                lefts.append(torch.from_numpy(l).to(dev))
+                rights.append(torch.from_numpy(r).to(dev))
+        outs = torch.empty((n, H, W), dtype=torch.float32, device=dev)
+        lp = [t.data_ptr() for t in lefts]
+        rp = [t.data_ptr() for t in rights]
+        op = [outs[i].data_ptr() for i in range(n)]
+        m = tsm.ADCensus(dev.index or 0)
+        m.setMatchingStrategy(tsm.ColorModel(model), False, False)
+        m.setMinMaxDisparity(0, D)
+        m.setOmpEmulation(omp)
+        m.setConcurrency(K)
+        m.compute_batch_device_ptr(lp, rp, H, W, W * 3, op, W * 4)
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(reps):
+            m.compute_batch_device_ptr(lp, rp, H, W, W * 3, op, W * 4)
+        torch.cuda.synchronize()
+        dt = time.perf_counter() - t0
+        got0 = np.ascontiguousarray(outs[0].cpu().numpy(), dtype=np.float32)
+        g = gold.get(key)
+        verified = g is not None and hashlib.sha256(got0.tobytes()).hexdigest() == g["sha256"]
+        # one frame at a time, device-resident images (single-frame latency)
+        m.setConcurrency(1)
+        m.compute_device_ptr(lp[0], rp[0], H, W, W * 3, op[0], W * 4)
+        m.synchronize()
+        t1 = time.perf_counter()
+        for i in range(5):
+            m.compute_device_ptr(lp[i % n], rp[i % n], H, W, W * 3, op[i % n], W * 4)
+            m.synchronize()
+        single = (time.perf_counter() - t1) / 5 * 1e3
+        # the cost walk alone: groups of one, HIP events around each launch
+        m.setProfiling(True)
+        m.resetStageTimes()
+        k = min(n, 8)
+        m.compute_batch_device_ptr(lp[:k], rp[:k], H, W, W * 3, op[:k], W * 4)
+        torch.cuda.synchronize()
+        m.setProfiling(False)
+        st = m.stageTimes()
+        m.close()
+        cost_ms, cost_n = st["cost"]
+        t_cost = cost_ms / max(1, cost_n) / 1e3
+        b_build = 4 * L * H * W * 2 + 2 * 3 * H * W
+        ach = b_build / t_cost / 1e9 if t_cost > 0 else None
+        res[name] = {
+            "workload": desc, "pairs": n, "concurrency": K,
+            "pairs_per_s": round(n * reps / dt, 3), "ms_per_frame": round(dt / (n * reps) * 1e3, 3),
+            "single_frame_device_ms": round(single, 3),
+            "cost_walk": {"avg_launch_ms": round(t_cost * 1e3, 4), "algorithmic_bytes": b_build,
+                          "achieved_GBps": round(ach, 1) if ach else None,
+                          "frac": round(ach / HBM_PEAK_GBS, 4) if ach else None, "launches": cost_n},
+            "stage_ms_per_pair": {kk: round(v[0] / max(1, v[1]), 4) for kk, v in st.items()},
+            "verified": bool(verified),
+            "verification": f"pair 0 (seed {seed0}) SHA-256 == oracle's ({key})" if g else f"no golden hash {key}",
+        }
+        del outs, lefts, rights
+        torch.cuda.empty_cache()
+    res["timing"] = (f"device batch entry, {reps} batches after one warm-up (wall clock, synchronised); "
+                     "single frame = mean of 5 device-resident compute() calls; cost walk = HIP events, groups of one")
+    return res
 
 
 def verify_outputs(m, tsm, outs, lefts, rights, seeds, H, W, D):

@@ -117,14 +117,29 @@ OPS_SIGNATURES = {
 }
 
 _lib = None
+LOADED_PATH = None  # the library file this process loaded (bench.py records it)
+
+
+def library_path() -> str:
+    """The product library, or -- for same-box A/B timing of a `make exp` build only -- the
+    file TSM_EXPERIMENT_LIB names.  Overridden loads print a warning on stderr and are
+    recorded in bench.py's line (`library`), so no result silently comes from another build."""
+    override = os.environ.get("TSM_EXPERIMENT_LIB")
+    if override:
+        import sys
+
+        print(f"[tea_stereo_matching_amd] WARNING: TSM_EXPERIMENT_LIB loads {override} instead of "
+              f"{LIB_PATH}", file=sys.stderr)
+        return override
+    return LIB_PATH
 
 
 def load() -> ctypes.CDLL:
     """Load the HIP library (raises if it has not been built: no CPU fallback)."""
-    global _lib
+    global _lib, LOADED_PATH
     if _lib is not None:
         return _lib
-    path = os.environ.get("TSM_LIB", LIB_PATH)  # developer hook: an experimental build
+    path = library_path()
     if not os.path.exists(path):
         raise ImportError(
             f"{path} not found: build the gfx950 library first "
@@ -142,6 +157,7 @@ def load() -> ctypes.CDLL:
         fn.restype = res
         fn.argtypes = args
     _lib = lib
+    LOADED_PATH = os.path.abspath(path)
     return lib
 
 

@@ -19,6 +19,7 @@
 #include <cstring>
 #include <functional>
 #include <limits>
+#include <map>
 #include <mutex>
 #include <string>
 #include <thread>
@@ -32,17 +33,28 @@
 using namespace tsm;
 
 namespace tsm {
-static int g_trace = -1;
 void trace_point(const char* what, hipStream_t st) {
-    if (g_trace < 0) {
+    static const bool trace = [] {  // read once (thread-safe static initialisation)
         const char* e = std::getenv("TSM_TRACE");
-        g_trace = (e && e[0] == '1') ? 1 : 0;
-    }
-    if (!g_trace) return;
+        return e && e[0] == '1';
+    }();
+    if (!trace) return;
     hipError_t le = hipGetLastError();
     hipError_t se = hipStreamSynchronize(st);
     std::fprintf(stderr, "[tsm] %-40s launch=%s sync=%s\n", what, hipGetErrorString(le), hipGetErrorString(se));
     std::fflush(stderr);
+}
+
+void ensure_lds_limit(const void* kernel, size_t bytes) {
+    static std::mutex mu;
+    static std::map<std::pair<const void*, int>, size_t> set;  // (kernel, device) -> limit set
+    int dev = 0;
+    (void)hipGetDevice(&dev);
+    std::lock_guard<std::mutex> g(mu);
+    size_t& cur = set[{kernel, dev}];
+    if (bytes <= cur) return;
+    if (hipFuncSetAttribute(kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes) == hipSuccess)
+        cur = bytes;
 }
 }  // namespace tsm
 
@@ -146,6 +158,7 @@ struct tsm_adc {
     tsm_adc_params params{};
     int omp_threads = 0;
     int concurrency = 2;
+    int ncu = 256;           // compute units of `device` (persistent-grid sizes)
     bool profiling = false;
     double stage_ms[TSM_STAGE_COUNT] = {};
     int stage_cnt[TSM_STAGE_COUNT] = {};
@@ -355,6 +368,7 @@ DevParams make_params(const tsm_adc* h, int H, int W) {
     P.maxD = h->max_disparity;
     P.L = P.maxD - P.minD + 1;
     P.Lp = round_up4(P.L);
+    P.ncu = h->ncu;
     P.color_model = h->color_model;
     P.mask = h->mask;
     P.censusW = p.census_win == 1 ? 7 : 9;
@@ -819,6 +833,9 @@ int tsm_adc_create(int device, tsm_adc** out) {
     if (device < 0 || device >= n) return TSM_ERR_ARGUMENT;
     tsm_adc* h = new tsm_adc();
     h->device = device;
+    int ncu = 0;
+    if (hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, device) == hipSuccess && ncu > 0)
+        h->ncu = ncu;
     default_params(&h->params, h->color_model);
     *out = h;
     return TSM_OK;

@@ -796,20 +796,9 @@ static size_t agg_split_lds(int qs) {
 }
 constexpr size_t kLdsBytes = 160 * 1024;
 
-template <bool FUSED>
-static void agg_stream_attrs() {
-    (void)hipFuncSetAttribute((const void*)k_agg_stream<FUSED, 0>, hipFuncAttributeMaxDynamicSharedMemorySize, kLdsBytes);
-    (void)hipFuncSetAttribute((const void*)k_agg_stream<FUSED, 49>, hipFuncAttributeMaxDynamicSharedMemorySize, kLdsBytes);
-}
-
 template <bool FUSED, int QT, bool BIG>
 static void launch_split_t(const AggStream& S, const DevParams& P, dim3 grid, size_t lds, hipStream_t st) {
-    static bool attr = false;
-    if (!attr) {
-        (void)hipFuncSetAttribute((const void*)k_agg_split<FUSED, QT, BIG>,
-                                  hipFuncAttributeMaxDynamicSharedMemorySize, kLdsBytes);
-        attr = true;
-    }
+    ensure_lds_limit((const void*)k_agg_split<FUSED, QT, BIG>, kLdsBytes);
     hipLaunchKernelGGL((k_agg_split<FUSED, QT, BIG>), grid, dim3(AX_THREADS), lds, st, S, P);
 }
 
@@ -822,11 +811,7 @@ static int launch_wholeline(float* vol, const uint32_t* arms, const int32_t* ws,
     qs = qs > Q ? Q : qs;
     const int nsl = (Q + qs - 1) / qs;
     qs = (Q + nsl - 1) / nsl;  // balanced slices
-    static bool attr = false;
-    if (!attr) {
-        (void)hipFuncSetAttribute((const void*)k_agg_wholeline, hipFuncAttributeMaxDynamicSharedMemorySize, kLdsBytes);
-        attr = true;
-    }
+    ensure_lds_limit((const void*)k_agg_wholeline, kLdsBytes);
     const dim3 g(2 * (horizontal ? P.H : P.W), nsl, P.npairs);
     hipLaunchKernelGGL(k_agg_wholeline, g, dim3(AL_THREADS), (size_t)n * qs * 16, st, vol, arms, ws, horizontal, qs, P);
     trace_point("k_agg_wholeline", st);
@@ -859,12 +844,7 @@ int launch_aggregation_pass(float* vol, const uint32_t* arms, const int32_t* ws,
     S.cpl = (S.n + AS_SEG - 1) / AS_SEG;
     S.nlv = horizontal ? P.H : P.W;
     S.nl = 2 * S.nlv;
-    static const int ncu = [] {
-        int dev = 0, n = 0;
-        (void)hipGetDevice(&dev);
-        (void)hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev);
-        return n > 0 ? n : 256;
-    }();
+    const int ncu = P.ncu;
     const int G = S.nl < ncu ? S.nl : ncu;
     // fused pass pairs: the role-split streamer (v6); single passes: v5 where its rings fit
     // (v6 for single passes too measured 1 % fewer pairs/s: round 3, same box)
@@ -884,15 +864,15 @@ int launch_aggregation_pass(float* vol, const uint32_t* arms, const int32_t* ws,
         trace_point(fused ? "k_agg_split<fused>" : "k_agg_split", st);
         return 0;
     }
-    static bool attr_set = false;
-    if (!attr_set) {
-        agg_stream_attrs<false>();
-        attr_set = true;
-    }
     const size_t lds = agg_stream_lds(P, false);
     const dim3 grid(G, 1, P.npairs), block(AS_THREADS);
-    if (Q == 49) hipLaunchKernelGGL((k_agg_stream<false, 49>), grid, block, lds, st, S, P);
-    else hipLaunchKernelGGL((k_agg_stream<false, 0>), grid, block, lds, st, S, P);
+    if (Q == 49) {
+        ensure_lds_limit((const void*)k_agg_stream<false, 49>, kLdsBytes);
+        hipLaunchKernelGGL((k_agg_stream<false, 49>), grid, block, lds, st, S, P);
+    } else {
+        ensure_lds_limit((const void*)k_agg_stream<false, 0>, kLdsBytes);
+        hipLaunchKernelGGL((k_agg_stream<false, 0>), grid, block, lds, st, S, P);
+    }
     trace_point("k_agg_stream", st);
     return 0;
 }

@@ -594,6 +594,7 @@ static void launch_cost_t(const uint32_t* desc, const float* lutA, int lutA_n, c
     // whole multiples of the 8 XCDs per pair, so every pair's blocks keep the same
     // block -> XCD dealing (the unit remap in the kernel relies on it)
     dim3 g(((units + wpb - 1) / wpb + 7) / 8 * 8, 1, P.npairs);
+    ensure_lds_limit((const void*)k_cost_walk<E, HSI, MASK>, cost_volume_lds_bytes(P));
     hipLaunchKernelGGL((k_cost_walk<E, HSI, MASK>), g, dim3(CW_THREADS), cost_volume_lds_bytes(P), st, desc, lutA,
                        lutA_n, lutB, vol, P, CW_SEG, nseg, nsl);
     trace_point("k_cost_walk", st);

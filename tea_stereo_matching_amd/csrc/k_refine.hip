@@ -886,6 +886,7 @@ void launch_region_voting(RefineBufs& B, const uint32_t* arms0, int hf, const De
     // workgroup per quarter word of a full image's ranks measured 32 us a launch, most idle)
     const size_t lds = (size_t)8 * P.L * sizeof(int);  // a histogram per rank of a quarter word
     const int vd_blocks = 4 * std::max(16, 256 / std::max(1, P.npairs));
+    ensure_lds_limit((const void*)k_vote_decide_rank, lds + 4096);  // + its static rank list
     hipLaunchKernelGGL(k_vote_decide_rank, grid1d(vd_blocks, P), dim3(VD_THREADS), lds, st, B.dm, B.dtmp,
                        arms0, B.out_list, B.cvote, B.csamp, B.counts, B.vbits, nb, hf, P);
     trace_point("k_vote_decide_rank", st);

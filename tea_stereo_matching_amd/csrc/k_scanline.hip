@@ -558,12 +558,7 @@ static void launch_scan_help_t(float* vol, const uint8_t* grad, const uint32_t* 
                                int store_view1, const float* infvec, const DevParams& P, hipStream_t st) {
     constexpr int K = 16;
     const size_t lds = (size_t)SH_LINES * 2 * K * 1280;
-    static bool attr = false;
-    if (!attr) {
-        (void)hipFuncSetAttribute((const void*)k_scan_line<1, K, true, MASK, true, OMP, true>,
-                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-        attr = true;
-    }
+    ensure_lds_limit((const void*)k_scan_line<1, K, true, MASK, true, OMP, true>, lds);
     const dim3 g((P.H + SH_LINES - 1) / SH_LINES, 2, P.npairs);
     hipLaunchKernelGGL((k_scan_line<1, K, true, MASK, true, OMP, true>), g, dim3(2 * SH_LINES * 64), lds, st, vol,
                        grad, img, dir, wta, store_view1, infvec, P);

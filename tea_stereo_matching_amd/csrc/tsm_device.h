@@ -52,6 +52,7 @@ struct DevParams {
     // from blockIdx.z (kernels with a view axis: blockIdx.z = 2 * pair + view).
     size_t pstride;
     int npairs;
+    int ncu;           // compute units of the handle's device (persistent grids)
 };
 
 // Streaming store of a volume vector: non-temporal (nt), since nothing reads it back

@@ -12,6 +12,12 @@ namespace tsm {
 // after every launch and log the kernel name + status to stderr.  No-op otherwise.
 void trace_point(const char* what, hipStream_t st);
 
+// Raise `kernel`'s dynamic-LDS limit to `bytes` on the current device, once per (kernel,
+// device) and thread-safe (engine.cpp): handles on several threads may launch at once, and
+// the attribute is a per-device property.  Launchers of kernels that may ask for more than
+// 64 KB of dynamic LDS call it before every launch (a lookup under a mutex after the first).
+void ensure_lds_limit(const void* kernel, size_t bytes);
+
 // k_cost.hip
 // Every launcher runs its stage for the group's P.npairs pairs (DevParams.pstride apart).
 void launch_pack(const PairIn& in, size_t step, uint32_t* img, const DevParams& P, hipStream_t st);

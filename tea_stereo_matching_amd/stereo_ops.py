@@ -214,20 +214,31 @@ def _dev_batch(srcs, what):
     return srcs
 
 
-def applyColorMapBatch(disparities, colorMap=None, minVal=None, maxVal=None):
-    """applyColorMap over a list of (H, W) float32 device tensors (tsm_apply_colormap_batch_device):
-    per map the same image as applyColorMap; returns a list of (H, W, 3) uint8 tensors."""
+def applyColorMapBatch(disparities, *args):
+    """applyColorMap over a list of (H, W) float32 device tensors (tsm_apply_colormap_batch_device),
+    with applyColorMap's argument forms: (disparities, colorMap) or (disparities, minVal,
+    maxVal, colorMap); (disparities) alone uses JETColorMap().  Per map the same image as
+    applyColorMap; returns a list of (H, W, 3) uint8 tensors."""
     import torch
 
+    if len(args) == 0:
+        cmap, use_range, mn, mx = JETColorMap(), 0, 0.0, 0.0
+    elif len(args) == 1:
+        (cmap,), use_range, mn, mx = args, 0, 0.0, 0.0
+    elif len(args) == 3:
+        mn, mx, cmap = args
+        if mn is None or mx is None:
+            raise ValueError("applyColorMapBatch: minVal and maxVal must both be given")
+        use_range = 1
+    else:
+        raise TypeError("applyColorMapBatch(disparities[, colorMap]) or "
+                        "applyColorMapBatch(disparities, minVal, maxVal, colorMap)")
     ss = _dev_batch([_f32(d) for d in disparities], "applyColorMapBatch")
     H, W = ss[0].shape
-    lut = np.ascontiguousarray(np.asarray(JETColorMap() if colorMap is None else colorMap,
-                                          dtype=np.uint8).reshape(256, 3))
-    use_range = minVal is not None
+    lut = np.ascontiguousarray(np.asarray(cmap, dtype=np.uint8).reshape(256, 3))
     outs = [torch.empty((H, W, 3), dtype=torch.uint8, device=ss[0].device) for _ in ss]
-    rc = N.load().tsm_apply_colormap_batch_device(len(ss), _ptr_array(ss), H, W, 4 * W, _ptr(lut), int(use_range),
-                                                  float(minVal or 0.0), float(maxVal or 0.0), _ptr_array(outs),
-                                                  3 * W, _stream())
+    rc = N.load().tsm_apply_colormap_batch_device(len(ss), _ptr_array(ss), H, W, 4 * W, _ptr(lut), use_range,
+                                                  float(mn), float(mx), _ptr_array(outs), 3 * W, _stream())
     _check(_done(rc, True), "applyColorMapBatch")
     return outs
 
@@ -259,11 +270,21 @@ def reprojectTo3DBatch(disparities, focalLength: float, baseline: float, cx: flo
 
 
 def remapBatch(srcs, map1, map2):
-    """cv::remap INTER_LINEAR of a list of device images of one size through the same
-    CV_16SC2 + CV_16UC1 maps (tsm_remap_linear_fixed_batch_device)."""
+    """cv::remap INTER_LINEAR of a list of uint8 device images of one size through the same
+    CV_16SC2 + CV_16UC1 maps (tsm_remap_linear_fixed_batch_device): map1 int16 (H, W, 2),
+    map2 uint16/int16 (H, W), both on the images' device.  Float maps go through remap()."""
     import torch
 
     ss = _dev_batch(srcs, "remapBatch")
+    if ss[0].dtype != torch.uint8 or ss[0].dim() not in (2, 3):
+        raise ValueError("remapBatch: sources must be uint8 (H, W) or (H, W, C) device tensors")
+    if not (_is_dev(map1) and _is_dev(map2)) or map1.device != ss[0].device or map2.device != ss[0].device:
+        raise ValueError("remapBatch: map1 and map2 must be tensors on the sources' device")
+    if map1.dtype != torch.int16 or map2.dtype not in (torch.uint16, torch.int16):
+        raise ValueError("remapBatch: expects CV_16SC2 (int16) + CV_16UC1 (uint16) maps; "
+                         "use remap() for float32 maps")
+    if map1.dim() != 3 or map1.shape[2] != 2 or map2.dim() != 2 or tuple(map1.shape[:2]) != tuple(map2.shape):
+        raise ValueError("remapBatch: map1 must be (H, W, 2) and map2 (H, W) of the same H, W")
     C = 1 if ss[0].dim() == 2 else ss[0].shape[2]
     sh, sw = ss[0].shape[:2]
     m1, m2 = map1.contiguous(), map2.contiguous()

@@ -20,6 +20,9 @@ Cases:
                  (ADCensus.cpp:339-340), 641 labels
   MASK_HSI_0600  the same pair with maskMatching in the reference's default HSI model
                  (bgr2hsi with the hue-band filter blacks out the background, :1463-1470)
+  B_HSI_1000     config B pair 1000 in the reference's default HSI model (bench configs block)
+  B_OMP20_1000   config B pair 1000, RGB, with the racy-schedule emulation at T = 20 (the
+                 mode equal to the reference's shipped outputs; bench configs block)
 
     python tests/golden/make_config_hashes.py [--threads N] [--only C B_1000 ...]
 """
@@ -69,6 +72,8 @@ def cases():
            ("MASK_HSI_0600", _demo_0600, 640, {"color_model": O.HSI, "mask_matching": 1})]
     for s in B_SEEDS:
         out.append((f"B_{s}", (lambda s=s: syn.config_b(s)), 192, rgb))
+    out.append(("B_HSI_1000", lambda: syn.config_b(1000), 192, {"color_model": O.HSI}))
+    out.append(("B_OMP20_1000", lambda: syn.config_b(1000), 192, dict(rgb, scan_emulate_threads=20)))
     return out
 
 

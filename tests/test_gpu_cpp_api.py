@@ -1,5 +1,13 @@
-"""Compile and run the C++ API check (tests/cpp/test_stereo_api.cpp) on the GPU box; its
-disparity is then compared with the oracle's, bit for bit."""
+"""Compile and run the C++ API checks on the GPU box; each program's disparity is then
+compared with the oracle's, bit for bit.
+
+* tests/cpp/test_stereo_api.cpp: include/stereo.h without OpenCV (ImageView virtual),
+  plus the f2-f4 calls.
+* tests/cpp/test_stereo_api_cvmat.cpp: include/stereo.h with a cv::Mat on the include path
+  (tests/cpp/cvshim), so StereoMatching's pure virtual is the reference's
+  compute(const cv::Mat&, const cv::Mat&, cv::Mat&) (reference stereo.h:325-331) and the
+  matcher is called through a StereoMatching&, on ROI (non-continuous) inputs.
+"""
 import os
 import subprocess
 
@@ -10,14 +18,23 @@ from conftest import ROOT, host_threads
 
 pytestmark = pytest.mark.gpu
 
+LIB = os.path.join(ROOT, "tea_stereo_matching_amd", "lib")
 
-def test_cpp_stereo_api(tmp_path):
-    exe = str(tmp_path / "test_stereo_api")
-    lib = os.path.join(ROOT, "tea_stereo_matching_amd", "lib")
-    subprocess.run(["g++", "-std=c++20", "-O1", "-I", os.path.join(ROOT, "include"),
-                    os.path.join(ROOT, "tests", "cpp", "test_stereo_api.cpp"), "-o", exe,
-                    f"-L{lib}", "-ltsm_adcensus", f"-Wl,-rpath,{lib}", "-L/opt/rocm/lib",
-                    "-lamdhip64", "-Wl,-rpath,/opt/rocm/lib"], check=True)
+
+def compile_program(src, exe, opencv):
+    cmd = ["g++", "-std=c++20", "-O1", "-Wall", "-Werror", "-I", os.path.join(ROOT, "include")]
+    if opencv:
+        cmd += ["-I", os.path.join(ROOT, "tests", "cpp", "cvshim")]
+    cmd += [os.path.join(ROOT, "tests", "cpp", src), "-o", exe, f"-L{LIB}", "-ltsm_adcensus",
+            f"-Wl,-rpath,{LIB}", "-L/opt/rocm/lib", "-lamdhip64", "-Wl,-rpath,/opt/rocm/lib"]
+    subprocess.run(cmd, check=True)
+
+
+@pytest.mark.parametrize("src,opencv", [("test_stereo_api.cpp", False),
+                                        ("test_stereo_api_cvmat.cpp", True)])
+def test_cpp_stereo_api(tmp_path, src, opencv):
+    exe = str(tmp_path / "prog")
+    compile_program(src, exe, opencv)
     r = subprocess.run([exe, str(tmp_path)], capture_output=True, text=True, timeout=120)
     assert r.returncode == 0, r.stdout + r.stderr
     assert "OK" in r.stdout

@@ -110,6 +110,10 @@ WIDE = [
     (45, 10, 700, 0, 640, 0),   # L 641: two cost slices, three scanline vectors a lane
     (46, 8, 1100, 0, 1024, 0),  # L 1025: three cost slices, eight scanline vectors a lane
     (47, 12, 430, 7, 330, 1),   # minD > 0 past 256 labels, HSI
+    # the top of the accepted range: L 2048 (four cost slices, eight scanline vectors a
+    # lane, the voting decision's 64 KB histogram block) and L 1901 in HSI
+    (49, 8, 2100, 0, 2047, 0),
+    (50, 6, 1950, 0, 1900, 1),
 ]
 
 
@@ -384,6 +388,23 @@ def test_full_size_configs_bit_exact(matcher, tsm, cfg):
     d_g = np.ascontiguousarray(d_g, dtype=np.float32)
     assert list(d_g.shape) == gold["shape"]
     assert abs(float((d_g >= 0).mean()) - gold["valid_fraction"]) < 1e-12
+    assert hashlib.sha256(d_g.tobytes()).hexdigest() == gold["sha256"]
+
+
+@pytest.mark.parametrize("key,model,omp", [("B_HSI_1000", 1, 0), ("B_OMP20_1000", 0, 20)])
+def test_config_b_modes_full_size(matcher, tsm, key, model, omp):
+    """Config B pair 1000 in the reference's default HSI model, and in RGB with the T = 20
+    race emulation (the mode equal to the reference's shipped outputs): SHA-256 of the fp32
+    disparity == the oracle's (the bench's configs block checks the same hashes)."""
+    import hashlib
+    import json
+
+    gold = json.load(open(os.path.join(GOLDEN, "config_hashes.json")))[key]
+    left, right, _ = tsm.synthetic.config_b(1000)
+    d_g, _ = _gpu(matcher, tsm, left, right, model, 0, 192, omp=omp)
+    matcher.setOmpEmulation(0)
+    matcher.setMatchingStrategy(tsm.ColorModel.RGB)
+    d_g = np.ascontiguousarray(d_g, dtype=np.float32)
     assert hashlib.sha256(d_g.tobytes()).hexdigest() == gold["sha256"]
 
 

@@ -221,7 +221,7 @@ def test_group_forms_equal_single_calls(tsm, oracle):
     cols = tsm.applyColorMapBatch(dev, lut)
     for d, c in zip(ds, cols):
         assert np.array_equal(c.cpu().numpy(), oracle.apply_colormap_ex(d))
-    cols = tsm.applyColorMapBatch(dev, lut, 10.0, 150.0)
+    cols = tsm.applyColorMapBatch(dev, 10.0, 150.0, lut)
     for d, c in zip(ds, cols):
         assert np.array_equal(c.cpu().numpy(), oracle.apply_colormap_ex(d, min_val=10.0, max_val=150.0))
     for d, o in zip(ds, tsm.reprojectToDepthBatch(dev, 721.5, 0.54)):
@@ -294,3 +294,29 @@ def test_strided_and_offset_maps(tsm, oracle):
                                   equal_nan=True), (step, i)
             assert np.array_equal(xyz[i, :, :3 * W].cpu().numpy().reshape(H, W, 3),
                                   oracle.reproject_to_3d(d, 700.0, 0.5, 20.0, 11.0), equal_nan=True), (step, i)
+
+
+def test_group_forms_reject_bad_arguments(tsm):
+    """remapBatch refuses what it would otherwise reinterpret (float maps, float sources,
+    mismatched map shapes, host maps); applyColorMapBatch refuses a half-given range."""
+    import torch
+
+    imgs = [torch.zeros((8, 10, 3), dtype=torch.uint8, device="cuda") for _ in range(2)]
+    xy = torch.zeros((8, 10, 2), dtype=torch.int16, device="cuda")
+    fr = torch.zeros((8, 10), dtype=torch.int16, device="cuda")
+    assert len(tsm.remapBatch(imgs, xy, fr)) == 2
+    bad = [
+        (imgs, xy.float(), fr.float()),                       # float maps: remap() only
+        ([i.float() for i in imgs], xy, fr),                   # float sources
+        (imgs, xy, fr[:, :9].contiguous()),                    # map shapes differ
+        (imgs, xy.cpu(), fr.cpu()),                            # host maps
+        (imgs, xy[..., 0].contiguous(), fr),                   # map1 not (H, W, 2)
+    ]
+    for args in bad:
+        with pytest.raises(ValueError):
+            tsm.remapBatch(*args)
+    d = [torch.zeros((4, 5), dtype=torch.float32, device="cuda")]
+    with pytest.raises(ValueError):
+        tsm.applyColorMapBatch(d, 1.0, None, tsm.JETColorMap())
+    with pytest.raises(TypeError):
+        tsm.applyColorMapBatch(d, 1.0, tsm.JETColorMap())

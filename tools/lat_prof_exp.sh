@@ -5,7 +5,7 @@ set -u
 cd /tmp && export TMPDIR=/tmp && cd "${GRAFT_REPO_ROOT}"
 mkdir -p gpurun_out
 for x in default "$@"; do
-  if [ $x = default ]; then unset TSM_LIB; else export TSM_LIB=build/exp/$x/libtsm_adcensus.so; fi
+  if [ $x = default ]; then unset TSM_EXPERIMENT_LIB; else export TSM_EXPERIMENT_LIB=build/exp/$x/libtsm_adcensus.so; fi
   timeout -k 10 300 rocprofv3 --kernel-trace --output-format csv -d gpurun_out/lpe_$x -o run -- python3 tools/latency.py 1 > gpurun_out/lpe_$x.log 2>&1 || { echo "$x rc=$?"; tail -5 gpurun_out/lpe_$x.log; exit 1; }
   echo "== $x: $(grep device gpurun_out/lpe_$x.log)"
   python3 - gpurun_out/lpe_$x/run_kernel_trace.csv <<'PY'
