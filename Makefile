@@ -14,7 +14,7 @@ HIPFLAGS := --offload-arch=$(ARCH) -O3 -std=c++20 -fPIC -ffp-contract=off \
 HIP_SRCS := k_cost k_aggregate k_scanline k_refine k_stereo_ops
 CPP_SRCS := engine stereo_ops stereo_ops_api
 OBJS     := $(addprefix $(OBJ)/,$(addsuffix .o,$(HIP_SRCS) $(CPP_SRCS)))
-HDRS     := $(SRC)/tsm_device.h $(SRC)/tsm_launch.h include/tsm_adcensus.h include/stereo.h include/tsm_stereo_ops.h
+HDRS     := $(SRC)/copy_pool.h $(SRC)/tsm_device.h $(SRC)/tsm_launch.h include/tsm_adcensus.h include/stereo.h include/tsm_stereo_ops.h
 
 all: lib oracle probe
 
