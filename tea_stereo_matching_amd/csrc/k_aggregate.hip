@@ -246,7 +246,7 @@ __global__ __launch_bounds__(AS_THREADS) void k_agg_stream(AggStream S, DevParam
     const size_t aes = S.horizontal ? 1 : (size_t)W;
     const size_t als = S.horizontal ? (size_t)W : 1;
     const int shA = S.horizontal ? 16 : 0, shB = S.horizontal ? 24 : 8;
-    const int g = blockIdx.x, G = gridDim.x;
+    const int g = xcd_remap(blockIdx.x, gridDim.x), G = gridDim.x;
     const int my_lines = (S.nl - g + G - 1) / G;
     const int nch = my_lines * S.cpl;
     const uint32_t r1_off = 0;                                            // LDS byte offsets
@@ -531,7 +531,7 @@ __global__ __launch_bounds__(AX_THREADS) void k_agg_split(AggStream S, DevParams
     const size_t ls = S.horizontal ? (size_t)W * Lp : (size_t)Lp;          // floats per line step
     const size_t aes = S.horizontal ? 1 : (size_t)W;
     const size_t als = S.horizontal ? (size_t)W : 1;
-    const int g = blockIdx.x, G = gridDim.x;
+    const int g = xcd_remap(blockIdx.x, gridDim.x), G = gridDim.x;
     const int my_lines = (S.nl - g + G - 1) / G;
     const int nch = my_lines * S.cpl;
     const uint32_t r1_off = 0;                                            // LDS byte offsets

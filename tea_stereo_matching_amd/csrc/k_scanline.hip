@@ -307,7 +307,10 @@ __global__ __launch_bounds__(HELP ? 2 * SH_LINES * 64 : 256) void k_scan_line(fl
     const int lane = threadIdx.x & 63;
     static_assert(!HELP || (J == 1 && HORIZ && WTA), "the helper form is the single-vector WTA pass");
     const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    int line = HELP ? (int)blockIdx.x * SH_LINES + wv % SH_LINES : (int)blockIdx.x * 4 + wv;
+    // vertical passes: neighbouring column groups on one XCD (xcd_remap; the launcher pads
+    // gridDim.x to a multiple of 8, blocks past the image exit)
+    int line = HELP ? (int)blockIdx.x * SH_LINES + wv % SH_LINES
+                    : (HORIZ ? (int)blockIdx.x : xcd_remap(blockIdx.x, gridDim.x)) * 4 + wv;
     pair_shift(blockIdx.z, P.pstride, vol, grad, img, wta);  // infvec: shared, not per pair
     const int v = blockIdx.y;
     // HELP: every wave of the workgroup takes the same barriers, so a line past the image
@@ -579,7 +582,7 @@ static void launch_scan_help(float* vol, const uint8_t* grad, const uint32_t* im
 template <int J, int K, bool HORIZ, bool MASK, bool WTA>
 static void launch_scan_t(float* vol, const uint8_t* grad, const uint32_t* img, int dir, int32_t* wta,
                           int store_view1, const float* infvec, const DevParams& P, hipStream_t st) {
-    dim3 g(((HORIZ ? P.H : P.W) + 3) / 4, 2, P.npairs);
+    dim3 g(HORIZ ? (P.H + 3) / 4 : ((P.W + 3) / 4 + 7) / 8 * 8, 2, P.npairs);
     if (P.omp_threads > 1)
         hipLaunchKernelGGL((k_scan_line<J, K, HORIZ, MASK, WTA, true>), g, dim3(256), 0, st, vol, grad, img, dir,
                            wta, store_view1, infvec, P);

@@ -78,6 +78,18 @@ __device__ __forceinline__ f32x4 div_ws(f32x4 a, float b, float y) {
     return q;
 }
 
+// XCD-aware block order.  Workgroups are dealt round-robin to the 8 XCDs (flat block b runs
+// on XCD b % 8; with gridDim.x a multiple of 8, blockIdx.x % 8 is the XCD whatever y / z).
+// Mapping b -> (b % 8) * per + b / 8 gives each XCD a contiguous run of the index space, so
+// workgroups that run side by side on one XCD own neighbouring lines: the 64-B granules two
+// neighbouring pixel vectors share (a 784-B vector is not a granule multiple) are then
+// fetched once into that XCD's L2 instead of once by each of two XCDs.  A permutation of
+// [0, n); blocks past the last multiple of 8 keep their index.
+__device__ __forceinline__ int xcd_remap(int b, int n) {
+    const int per = n >> 3;
+    return b < 8 * per ? (b & 7) * per + (b >> 3) : b;
+}
+
 // Largest group a launch carries (pointer tables of per-pair user buffers are kernel
 // arguments of this many entries).
 constexpr int kMaxGroup = 64;
