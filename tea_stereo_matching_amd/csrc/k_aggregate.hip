@@ -17,6 +17,9 @@
 
 namespace tsm {
 
+#define TSM_STR2(x) #x
+#define TSM_STR(x) TSM_STR2(x)
+
 // computeLimit, ADCensus.cpp:604-659 (returns the arm length; one shorter when the walk
 // ends at the image border, :650-658).  p: the pixel; fetch(k): the pixel k steps along the
 // arm's direction; avail: how many such steps stay inside the image.
@@ -156,50 +159,39 @@ __global__ void k_color_grad(const uint32_t* __restrict__ img, uint8_t* __restri
 }
 
 // ---------------------------------------------------------------------------
-// 1-D aggregation v4: label-grouped streamer, optionally two passes fused
-// ---------------------------------------------------------------------------
-// 1-D aggregation v5: persistent line streamer, same-direction pass pairs fused
+// 1-D aggregation: persistent line streamer, same-direction pass pairs fused
 // ---------------------------------------------------------------------------
 // Each workgroup (one per CU) owns every G-th line of the pass (both views) and treats
 // them as ONE continuous pixel stream: windows never cross a line (arms stop at the
 // image border), so lines simply follow each other and there is no per-line warm-up.
-// The stream moves in chunks of AS_SEG pixels, one chunk per step.  Eight loader waves
-// stage chunk PAIRS in VGPRs (global_load_dwordx4; loader k % 8 owns pair k, one pair in
-// flight per loader = 16 chunks = ~100 KB per CU for config B) and copy a landed pair
-// into an LDS ring (ring1) AS_AHEAD steps before its first chunk is summed.  Each of the
-// AS_SEG summing waves produces one output per step with the reference's strictly
-// sequential window sum (lanes own float4 of labels).
+// The stream moves in chunks of AS_SEG pixels, one chunk per step; a chunk's pixel
+// vectors land in an LDS ring (ring1) AS_AHEAD steps before the chunk is summed, and each
+// pixel's window is summed with the reference's strictly sequential order (lanes own
+// float4 of labels).
 //   FUSED: pass A (the 2nd pass of an iteration, divided by the window sizes) writes
 //   its outputs to a second ring (ring2) and pass B (the 1st pass of the next
 //   iteration, same direction) sums them AS_LAG steps later, so the volume makes one
-//   HBM round trip for two passes.  Not fused: pass A's outputs go straight to HBM.
+//   HBM round trip for two passes.  Not fused (the first and the last pass): pass A's
+//   outputs are copied out of ring2 to HBM.
 // In place: a pixel is overwritten AS_AHEAD (+AS_LAG) steps after it was staged.
 // The per-pixel window sizes divide through an exact reciprocal-FMA quotient:
 // q0 = a*y, r = fma(-q0, b, a), q = fma(r, y, q0) with y = RN(1/b) equals RN(a/b) for
 // every integer b in [1, 6561] (arms up to 40) and every a in [2^-40, 2^16) (exhaustively checked,
 // tools/micro/div_check.c); smaller a take the IEEE division.
-#ifndef AS_GRP
-#define AS_GRP 1                            // chunks per loader turn
-#endif
-constexpr int AS_SEG = 8;                   // pixels per chunk = summing waves
-constexpr int AS_LOAD = 8;                  // loader waves (turn k: loader k % 8)
-constexpr int AS_THREADS = (AS_SEG + AS_LOAD) * 64;
+constexpr int AS_SEG = 8;                   // pixels per chunk = A waves = B waves
 constexpr int AS_AH = 5;                    // windows reach at most 5 chunks either side
 constexpr int AS_MAX_ARM = AS_AH * AS_SEG;
 constexpr int AS_AHEAD = AS_AH + 1;         // chunk c is readable from step c - AHEAD + 1
-constexpr int AS_RC1 = 2 * AS_AH + 1 + AS_GRP;  // ring1 chunks: 2*AH+1 read + a turn landing
+constexpr int AS_RC1 = 2 * AS_AH + 2;       // ring1 chunks: 2*AH+1 read + one landing
 constexpr int AS_RC2 = 2 * AS_AH + 2;       // ring2 chunks: 2*AH+1 read + one written
 constexpr int AS_RP1 = AS_RC1 * AS_SEG;
 constexpr int AS_RP2 = AS_RC2 * AS_SEG;
 constexpr int AS_LAG = AS_AH + 1;           // pass B at step s outputs chunk s - LAG
-constexpr int AS_MC = 16;                   // meta ring chunks (> AHEAD + GRP + LAG)
-static_assert(AS_AHEAD % AS_GRP == 0, "turns land on steps NG*k - AHEAD");
 
-// Cache policy of the single-pass streamer's volume loads (the first and the last pass):
-// streaming (slc).  Each vector is read once; the following scanline pass then ran 4 %
-// faster for a single pair (1.106 against 1.152 ms, same box, round 3) with the
-// aggregation unchanged.  The fused streamer keeps default loads (slc there: 1.55 against
-// 1.47 ms).
+// Cache policy of the single passes' volume loads (the first and the last pass):
+// streaming (slc).  Each vector is read once; the scanline pass after the last one then ran
+// 4 % faster for a single pair (1.106 against 1.152 ms, same box, round 3).  The fused
+// pass pairs keep default loads (slc there: 1.55 against 1.47 ms).
 constexpr int kNtLoad = 2;
 // raw buffer resource over p (gfx9 dword3: 32-bit data format, no swizzle); offsets are
 // unsigned 32-bit, the launcher checks that every line of a pass fits
@@ -211,10 +203,10 @@ struct AggStream {
     float* vol;
     const uint32_t* arms;
     const int32_t* ws;     // window sizes of the dividing pass (nullptr: no divide)
-    const uint32_t* pk;    // split streamer: packed descriptors of this direction, view 0
-    const float* rcp;      // split streamer: reciprocals of this direction, view 0
-    int qtot;              // split streamer: label vectors per pixel (Lp / 4)
-    int qn0;               // split streamer: label vectors per slice (blockIdx.y; the last may be narrower)
+    const uint32_t* pk;    // packed descriptors of this direction, view 0
+    const float* rcp;      // reciprocals of this direction, view 0
+    int qtot;              // label vectors per pixel (Lp / 4)
+    int qn0;               // label vectors per slice (blockIdx.y; the last may be narrower)
     int horizontal;
     int n;                 // pixels per line
     int cpl;               // chunks per line
@@ -222,280 +214,11 @@ struct AggStream {
     int nl;                // lines of both views
 };
 
-
-// Per-pixel window descriptor, precomputed by the loader when the pixel lands (so the
-// summing waves spend no scalar work on ring arithmetic): 32 B per pixel.
-//   [0] LDS byte offset of the pass-A window start in ring1   [1] window length
-//   [2] y = RN(1/windowSize)                                   [3] windowSize as float
-//   [4] LDS byte offset of the pass-B window start in ring2   [5] window length
-constexpr int AS_MW = 8;  // meta words per pixel
 constexpr int AX_MIR = 3;  // mirror slots after each ring (a 4-read block spans 3 slots past its start)
 
-// QT > 0: the pixel vector has QT float4 (compile-time ring stride); 0: runtime Q.
-template <bool FUSED, int QT>
-__global__ __launch_bounds__(AS_THREADS) void k_agg_stream(AggStream S, DevParams Pk) {
-    const DevParams P = Pk;
-    pair_shift(blockIdx.z, P.pstride, S.vol, S.arms, S.ws, S.pk, S.rcp);
-    extern __shared__ __attribute__((aligned(16))) f32x4 smem_f4[];
-    const int H = P.H, W = P.W, Lp = P.Lp;
-    const int Q = QT > 0 ? QT : Lp >> 2;
-    const uint32_t Qs = (uint32_t)Q * 16;                                // bytes per ring pixel
-    const size_t vstride = (size_t)H * W * Lp;
-    const size_t es = S.horizontal ? (size_t)Lp : (size_t)W * Lp;         // floats per pixel step
-    const size_t ls = S.horizontal ? (size_t)W * Lp : (size_t)Lp;          // floats per line step
-    const size_t aes = S.horizontal ? 1 : (size_t)W;
-    const size_t als = S.horizontal ? (size_t)W : 1;
-    const int shA = S.horizontal ? 16 : 0, shB = S.horizontal ? 24 : 8;
-    const int g = xcd_remap(blockIdx.x, gridDim.x), G = gridDim.x;
-    const int my_lines = (S.nl - g + G - 1) / G;
-    const int nch = my_lines * S.cpl;
-    const uint32_t r1_off = 0;                                            // LDS byte offsets
-    const uint32_t r2_off = (uint32_t)(AS_RP1 + AX_MIR) * Qs;  // each ring + AX_MIR mirror slots
-    const uint32_t meta_off = r2_off + (FUSED ? (uint32_t)(AS_RP2 + AX_MIR) * Qs : 0u);
-    char* lds = reinterpret_cast<char*>(smem_f4);
-
-    const int tid = threadIdx.x;
-    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-    const int lane = tid & 63;
-    const bool loader = wave >= AS_SEG;
-    const int li = wave - AS_SEG;
-    const int nsteps = nch + (FUSED ? AS_LAG : 0);
-    const uint32_t lane16 = (uint32_t)lane * 16;
-    const bool vl = lane < Q;
-    // float offset of pixel 0 of local line lidx
-    auto line_base = [&](int lidx) -> size_t {
-        const int gl = g + lidx * G;
-        const int v = gl / S.nlv, line = gl - v * S.nlv;
-        return (size_t)v * vstride + (size_t)line * ls;
-    };
-
-    if (loader) {
-        // ---- loader li: turns k = li, li + 8, ... (chunks NG*k .. NG*k+NG-1), one turn's
-        // chunks in flight (one buffer per wave: the compiler's wait before the copy is a
-        // plain vmcnt(0)).  Every load and LDS write is unconditional (lanes past the
-        // vector repeat lane Q-1): with no exec branches the compiler's waits stay at the
-        // copy (land) and never stall the next turn's issue.
-        constexpr int NG = AS_GRP;
-        f32x4 b[NG * AS_SEG];
-        uint32_t ma[NG], mw[NG];                   // meta of chunk NG*k+h (pixel lane & 7)
-        const int lanec = lane < Q ? lane : Q - 1;
-        int lidx = 0, cc = NG * li;                // stream position of chunk NG*k
-        while (cc >= S.cpl) { cc -= S.cpl; ++lidx; }
-        // Byte offsets of the lines a turn can touch (vol, arms, window sizes), rebuilt
-        // (one division) only when the turn moves to a new line.  Loads are buffer loads
-        // off kernel-wide resources: a shared lane offset (VGPR) plus a per-pixel scalar
-        // offset, so no 64-bit VGPR addresses compete with the staging buffer.
-        const __amdgpu_buffer_rsrc_t rs_vol = make_rsrc(S.vol), rs_arm = make_rsrc(S.arms),
-                                     rs_ws = make_rsrc(S.ws);
-        struct LineRes { int l; uint32_t vol, arm, ws; };
-        auto line_res = [&](int l) -> LineRes {
-            const int gl = g + l * G;
-            const int v = gl / S.nlv, line = gl - v * S.nlv;
-            const uint32_t a = (uint32_t)(v * H * W + line * (int)als);
-            return LineRes{l, (uint32_t)(((size_t)v * vstride + (size_t)line * ls) * 4), a * 4,
-                           (a + (uint32_t)(v * H * W)) * 4};  // ws: per-view stride 2HW
-        };
-        LineRes lr[NG];
-#pragma unroll
-        for (int h = 0; h < NG; ++h) lr[h] = line_res(0);
-        const int last_l = my_lines - 1, last_cc = S.cpl - 1;
-        const uint32_t voff = (uint32_t)lanec * 16;
-        const uint32_t es4 = (uint32_t)(es * 4), aes4 = (uint32_t)(aes * 4);
-        const uint32_t mpx = (uint32_t)(lane & 7);
-        auto issue = [&]() {  // the turn at (lidx, cc): chunk NG*k and its successors
-            int l[NG], c[NG];
-            l[0] = lidx; c[0] = cc;
-#pragma unroll
-            for (int h = 1; h < NG; ++h) {
-                l[h] = c[h - 1] + 1 == S.cpl ? l[h - 1] + 1 : l[h - 1];
-                c[h] = c[h - 1] + 1 == S.cpl ? 0 : c[h - 1] + 1;
-            }
-#pragma unroll
-            for (int h = 0; h < NG; ++h) {
-                if (l[h] > last_l) { l[h] = last_l; c[h] = last_cc; }  // past the end: re-read
-                if (lr[h].l != l[h]) lr[h] = (h && lr[h - 1].l == l[h]) ? lr[h - 1] : line_res(l[h]);
-            }
-            // meta first: a wait the compiler places before a meta load then finds no
-            // vector load of this turn in flight yet
-#pragma unroll
-            for (int h = 0; h < NG; ++h) {  // every lane loads (pixel lane & 7): no exec branches
-                const uint32_t pos = min((uint32_t)c[h] * AS_SEG + mpx, (uint32_t)S.n - 1);
-                ma[h] = (uint32_t)__builtin_amdgcn_raw_buffer_load_b32(rs_arm, pos * aes4, lr[h].arm, 0);
-                mw[h] = S.ws ? (uint32_t)__builtin_amdgcn_raw_buffer_load_b32(rs_ws, pos * aes4, lr[h].ws, 0) : 1u;
-            }
-#pragma unroll
-            for (int h = 0; h < NG; ++h) {
-                const int p0 = c[h] * AS_SEG;
-#pragma unroll
-                for (int i = 0; i < AS_SEG; ++i) {
-                    const uint32_t pos = (uint32_t)min(p0 + i, S.n - 1);
-                    b[h * AS_SEG + i] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rs_vol, voff, lr[h].vol + pos * es4, kNtLoad));
-                }
-            }
-        };
-        auto land = [&](int k) {
-#pragma unroll
-            for (int h = 0; h < NG; ++h) {
-                const int c = NG * k + h;
-                char* slot = lds + r1_off + (uint32_t)(c % AS_RC1) * AS_SEG * Qs + (uint32_t)lanec * 16;
-#pragma unroll
-                for (int i = 0; i < AS_SEG; ++i) *reinterpret_cast<f32x4*>(slot + i * Qs) = b[h * AS_SEG + i];
-                if (c % AS_RC1 == 0) {  // ring slots 0..AX_MIR-1 are mirrored past the ring's end
-#pragma unroll
-                    for (int i = 0; i < AX_MIR; ++i)
-                        *reinterpret_cast<f32x4*>(slot + (AS_RP1 + i) * Qs) = b[h * AS_SEG + i];
-                }
-            }
-            if (lane < NG * AS_SEG) {  // window descriptors of the turn's pixels
-                const int hh = lane >> 3, c = NG * k + hh, px = lane & 7;
-                uint32_t a = ma[0], wsz = mw[0];
-#pragma unroll
-                for (int h = 1; h < NG; ++h)
-                    if (hh == h) { a = ma[h]; wsz = mw[h]; }
-                const int lo = (a >> shA) & 0xff, hi = (a >> shB) & 0xff;
-                const float bw = (float)(int)wsz;
-                const int rp1 = (c % AS_RC1) * AS_SEG + px;
-                const int rp2 = (c % AS_RC2) * AS_SEG + px;
-                uint32_t* m = reinterpret_cast<uint32_t*>(lds + meta_off) + ((c % AS_MC) * AS_SEG + px) * AS_MW;
-                m[0] = r1_off + (uint32_t)((rp1 - lo + AS_RP1) % AS_RP1) * Qs;
-                m[1] = (uint32_t)(lo + hi + 1);
-                m[2] = __float_as_uint(1.0f / bw);
-                m[3] = __float_as_uint(bw);
-                m[4] = r2_off + (uint32_t)((rp2 - lo + AS_RP2) % AS_RP2) * Qs;
-                m[5] = (uint32_t)(lo + hi + 1);
-            }
-        };
-        auto advance = [&]() {  // to the loader's next turn: NG * AS_LOAD chunks on
-            cc += NG * AS_LOAD;
-            while (cc >= S.cpl) { cc -= S.cpl; ++lidx; }
-        };
-        // prologue: turn li in flight; turns with chunks < AHEAD land before step 0
-        issue();
-        if (NG * li < AS_AHEAD) {
-            land(li);
-            advance();
-            issue();
-        }
-        asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
-        for (int t = 0; t < nsteps; ++t) {
-            // turn k lands during step NG*k - AHEAD
-            const int k = (t + AS_AHEAD) / NG;
-            if ((t + AS_AHEAD) % NG == 0 && (k & (AS_LOAD - 1)) == li && NG * k < nch) {
-                land(k);
-                advance();
-                issue();
-            }
-            asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
-        }
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // no load outlives the workgroup
-        return;
-    }
-
-    // ---- summing waves -------------------------------------------------------------
-    // Sequential window sum of `len` ring pixels from LDS byte offset `off` in the ring
-    // [rb, re): whole blocks of 4 at immediate offsets (AX_MIR mirror slots past each ring
-    // make every block contiguous), then the 1-3 remaining pixels under uniform branches.
-    auto window = [&](uint32_t off, int len, uint32_t rb, uint32_t re) -> f32x4 {
-        f32x4 acc = f32x4{0.f, 0.f, 0.f, 0.f};
-        const char* lp = lds + lane16;
-        const uint32_t span = re - rb;
-        for (int nb = len >> 2; nb > 0; --nb) {
-            const char* p = lp + off;
-            const f32x4 x0 = *reinterpret_cast<const f32x4*>(p);
-            const f32x4 x1 = *reinterpret_cast<const f32x4*>(p + Qs);
-            const f32x4 x2 = *reinterpret_cast<const f32x4*>(p + 2 * Qs);
-            const f32x4 x3 = *reinterpret_cast<const f32x4*>(p + 3 * Qs);
-            acc += x0;
-            acc += x1;
-            acc += x2;
-            acc += x3;
-            off += 4 * Qs;
-            off = off >= re ? off - span : off;
-        }
-        const int r = len & 3;
-        if (r) {
-            const char* p = lp + off;
-            const f32x4 x0 = *reinterpret_cast<const f32x4*>(p);
-            const f32x4 x1 = *reinterpret_cast<const f32x4*>(p + Qs);
-            const f32x4 x2 = *reinterpret_cast<const f32x4*>(p + 2 * Qs);
-            acc += x0;
-            if (r > 1) acc += x1;
-            if (r > 2) acc += x2;
-        }
-        return acc;
-    };
-    // output position of chunk `c`'s pixel `wave`: running float offset, new line: one division
-    struct Out {
-        int lidx, cc;
-        size_t off;
-    };
-    auto out_init = [&](Out& o) { o.lidx = 0; o.cc = 0; o.off = line_base(0) + (size_t)wave * es; };
-    auto out_step = [&](Out& o) {
-        if (++o.cc == S.cpl) { o.cc = 0; ++o.lidx; if (o.lidx < my_lines) o.off = line_base(o.lidx) + (size_t)wave * es; }
-        else o.off += (size_t)AS_SEG * es;
-    };
-    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");  // prologue chunks landed
-    Out oa, ob;
-    out_init(oa);
-    out_init(ob);
-    const uint32_t mstep = AS_SEG * AS_MW * 4, mwrap = AS_MC * mstep;
-    const uint32_t* mbase = reinterpret_cast<const uint32_t*>(lds + meta_off + (uint32_t)wave * AS_MW * 4);
-    uint32_t ma_off = 0;                                            // meta of chunk s (pass A)
-    uint32_t mb_off = (uint32_t)((AS_MC - AS_LAG) % AS_MC) * mstep; // meta of chunk s - LAG (pass B)
-    uint32_t r2w = r2_off + (uint32_t)wave * Qs;                   // ring2 slot of chunk s
-    // descriptors are read one step ahead (they landed AHEAD steps before use)
-    u32x4 mA = *reinterpret_cast<const u32x4*>(reinterpret_cast<const char*>(mbase) + ma_off);
-    uint2 mB = *reinterpret_cast<const uint2*>(reinterpret_cast<const char*>(mbase) + mb_off + 16);
-    for (int s = 0; s < nsteps; ++s) {
-        const uint32_t a_off = __builtin_amdgcn_readfirstlane(mA.x);
-        const int a_len = (int)__builtin_amdgcn_readfirstlane(mA.y);
-        const float a_y = __uint_as_float(__builtin_amdgcn_readfirstlane(mA.z));
-        const float a_b = __uint_as_float(__builtin_amdgcn_readfirstlane(mA.w));
-        const uint32_t b_off = __builtin_amdgcn_readfirstlane(mB.x);
-        const int b_len = (int)__builtin_amdgcn_readfirstlane(mB.y);
-        ma_off += mstep;
-        ma_off = ma_off >= mwrap ? ma_off - mwrap : ma_off;
-        mb_off += mstep;
-        mb_off = mb_off >= mwrap ? mb_off - mwrap : mb_off;
-        mA = *reinterpret_cast<const u32x4*>(reinterpret_cast<const char*>(mbase) + ma_off);
-        mB = *reinterpret_cast<const uint2*>(reinterpret_cast<const char*>(mbase) + mb_off + 16);
-        const uint32_t r1_end = r1_off + (uint32_t)AS_RP1 * Qs, r2_end = r2_off + (uint32_t)AS_RP2 * Qs;
-        // pass B first: it reads ring2 slots pass A does not write this step, so pass A's
-        // ring1 reads can overlap it
-        if (FUSED && s >= AS_LAG) {  // pass B on chunk s - LAG
-            if (ob.cc * AS_SEG + wave < S.n) {
-                const f32x4 acc = window(b_off, b_len, r2_off, r2_end);
-                if (vl) st_stream(S.vol + ob.off + 4 * lane, acc);
-            }
-            out_step(ob);
-        }
-        if (s < nch) {  // pass A on chunk s
-            if (oa.cc * AS_SEG + wave < S.n) {
-                f32x4 acc = window(a_off, a_len, r1_off, r1_end);
-                if (S.ws) acc = div_ws(acc, a_b, a_y);
-                if (FUSED) {
-                    if (vl) {
-                        *reinterpret_cast<f32x4*>(lds + r2w + lane16) = acc;
-                        if (r2w < r2_off + (uint32_t)AX_MIR * Qs)
-                            *reinterpret_cast<f32x4*>(lds + r2w + (uint32_t)AS_RP2 * Qs + lane16) = acc;
-                    }
-                } else if (vl) {
-                    st_stream(S.vol + oa.off + 4 * lane, acc);
-                }
-            }
-            out_step(oa);
-            r2w += AS_SEG * Qs;
-            r2w = r2w >= r2_end ? r2w - (uint32_t)AS_RP2 * Qs : r2w;
-        }
-        asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
-    }
-}
-
 // ---------------------------------------------------------------------------
-// 1-D aggregation v6: role-split persistent streamer (the default)
-// ---------------------------------------------------------------------------
-// Same stream, rings and window descriptors as v5, but the 16 waves of a workgroup split
-// by role so a step's two window sums run in parallel and no wave ever mixes loads with
+// The streamer's 16 waves split by role, so a step's two window sums run in parallel and
+// no wave ever mixes loads with
 // stores (the compiler drains vmcnt(0) whenever a wave with stores in flight consumes a
 // load):
 //   A waves (8): wave w owns pixel w of every chunk.  It stages its own pixel vectors
@@ -505,17 +228,37 @@ __global__ __launch_bounds__(AS_THREADS) void k_agg_stream(AggStream S, DevParam
 //   B waves (8): pass B of chunk s - LAG over ring2 (FUSED), or the copy of pass A's
 //     chunk s - 1 out of ring2 (single pass), and the stores to HBM.
 // One barrier per step; every wave runs the same whole number of AX_D-step blocks.
+//
+// Scalar work: one workgroup fills a CU (16 waves, 4 a SIMD) and a CU issues about one
+// scalar instruction a cycle, so per-step scalar bookkeeping of 16 waves sets the step's
+// floor (round 4: ~85 SALU a wave and step in the ISA of the previous form, SQ_INSTS_SALU
+// 1.7x SQ_INSTS_VALU).  Per-pixel bookkeeping is therefore vector work done once a block
+// of AX_D steps, lane k for the block's k-th chunk:
+//   * issue positions (line, chunk, volume offset) and the pixels' packed arms / window
+//     sizes / reciprocals (one per-lane load each, a block ahead of use);
+//   * the window descriptors of the block's landing chunks (ring offsets of both passes,
+//     length, divisor and reciprocal, the pixel's volume offset), written to a meta ring of
+//     2 * AX_D chunks, so a step only reads its descriptor (v_readfirstlane);
+//   * the window loops keep their ring offset in a VGPR (wrap by v_cndmask).
 constexpr int AX_THREADS = 16 * 64;
-constexpr int AX_MW = 2;  // meta words per pixel: packed descriptor (lo, hi, size), RN(1/size)
-constexpr int AX_D = 12;  // A-wave staging ring: steps in flight (AX_D * 8 px * Q * 16 B per CU)
-constexpr int AX_MC = 12;  // meta ring chunks (B reads chunk s - LAG + 1 before A overwrites its slot)
-static_assert(AX_D == AS_RC1 && AX_D == AS_RC2 && AX_D == AX_MC, "ring slots are compile-time per unrolled step");
-static_assert(AS_AHEAD + AS_LAG <= AX_MC, "meta ring too short for the B lag");
+constexpr int AX_MW = 8;   // meta words per pixel (32 B): see k_agg_split
+constexpr int AX_D = 12;   // A-wave staging ring: steps in flight (AX_D * 8 px * Q * 16 B per CU)
+constexpr int AX_MC = 2 * AX_D;  // meta ring chunks: a block's descriptors are written at its start
+static_assert(AX_D == AS_RC1 && AX_D == AS_RC2, "ring slots are compile-time per unrolled step");
+static_assert(AS_AHEAD + AS_LAG <= AX_D, "meta ring too short for the B lag");
+static_assert(AS_RP1 == AS_RP2, "pass B's ring2 window starts at pass A's ring1 slot");
 
-// BIG: volumes of 2 GiB and more (configs C, E): vector loads through 64-bit addresses
-// instead of 32-bit buffer offsets.  Label slices: when a pixel vector's rings would not fit
-// the CU's LDS, blockIdx.y picks one slice of the label axis (the sums of different labels
-// are independent), each a narrower ring.
+// BIG: volumes of 2 GiB and more (configs C, E): vector loads and stores through 64-bit
+// addresses instead of 32-bit buffer offsets.  Label slices: when a pixel vector's rings
+// would not fit the CU's LDS, blockIdx.y picks one slice of the label axis (the sums of
+// different labels are independent), each a narrower ring.
+//
+// Meta of pixel w of chunk c (slot c % AX_MC), written by A wave w at the start of the block
+// in which the pixel lands:
+//   [0] LDS byte offset of the pass-A window start in ring1 (pass B: + ring2 - ring1)
+//   [1] window length, 0 = no output (past the line or the workgroup's stream)
+//   [2] RN(1/windowSize) bits   [3] windowSize as float
+//   [4] the pixel's volume byte offset from the slice base, low word   [5] high word
 template <bool FUSED, int QT, bool BIG>
 __global__ __launch_bounds__(AX_THREADS) void k_agg_split(AggStream S, DevParams Pk) {
     const DevParams P = Pk;
@@ -529,8 +272,8 @@ __global__ __launch_bounds__(AX_THREADS) void k_agg_split(AggStream S, DevParams
     const size_t vstride = (size_t)H * W * Lp;
     const size_t es = S.horizontal ? (size_t)Lp : (size_t)W * Lp;         // floats per pixel step
     const size_t ls = S.horizontal ? (size_t)W * Lp : (size_t)Lp;          // floats per line step
-    const size_t aes = S.horizontal ? 1 : (size_t)W;
-    const size_t als = S.horizontal ? (size_t)W : 1;
+    const uint32_t aes = S.horizontal ? 1u : (uint32_t)W;
+    const uint32_t als = S.horizontal ? (uint32_t)W : 1u;
     const int g = xcd_remap(blockIdx.x, gridDim.x), G = gridDim.x;
     const int my_lines = (S.nl - g + G - 1) / G;
     const int nch = my_lines * S.cpl;
@@ -551,22 +294,29 @@ __global__ __launch_bounds__(AX_THREADS) void k_agg_split(AggStream S, DevParams
     const int nblk = (nsteps + AX_D - 1) / AX_D;  // every wave runs nblk * AX_D steps
     const uint32_t lane16 = (uint32_t)lane * 16;
     const bool vl = lane < Q;
-    auto line_base = [&](int lidx) -> size_t {
-        const int gl = g + lidx * G;
-        const int v = gl / S.nlv, line = gl - v * S.nlv;
-        return (size_t)v * vstride + (size_t)line * ls;
+#ifdef TSM_EXP_AGG_SALU  // timing probe (make exp): TSM_EXP_AGG_SALU extra scalar adds a step and wave
+    auto barrier = [&]() {
+        uint32_t d;
+        asm volatile("s_mov_b32 %0, 0\n.rept " TSM_STR(TSM_EXP_AGG_SALU) "\ns_add_u32 %0, %0, 1\n.endr" : "=s"(d));
+        asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
     };
+#elif defined(TSM_EXP_AGG_NOBARRIER)  // timing probe (make exp): no per-step barrier (wrong results)
+    auto barrier = [&]() { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); };
+#else
     auto barrier = [&]() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); };
+#endif
     // sequential window sum of `len` ring pixels from LDS byte offset `off` (a slot of the
     // ring [rb, re)): whole blocks of 4 at immediate offsets (the mirror slots make every
     // block contiguous), then the 1-3 remaining pixels under uniform branches -- the
-    // reference's order, no padding reads, little scalar bookkeeping
+    // reference's order, no padding reads.  The running offset is a VGPR (its wrap a
+    // v_cndmask): only the block count is scalar.
     auto window = [&](uint32_t off, int len, uint32_t rb, uint32_t re) -> f32x4 {
         f32x4 acc = f32x4{0.f, 0.f, 0.f, 0.f};
-        const char* lp = lds + lane16;
+        uint32_t vo = off;
+        asm volatile("" : "+v"(vo));  // a vector value from here on
         const uint32_t span = re - rb;
         for (int nb = len >> 2; nb > 0; --nb) {
-            const char* p = lp + off;
+            const char* p = lds + vo + lane16;
             const f32x4 x0 = *reinterpret_cast<const f32x4*>(p);
             const f32x4 x1 = *reinterpret_cast<const f32x4*>(p + Qs);
             const f32x4 x2 = *reinterpret_cast<const f32x4*>(p + 2 * Qs);
@@ -575,12 +325,12 @@ __global__ __launch_bounds__(AX_THREADS) void k_agg_split(AggStream S, DevParams
             acc += x1;
             acc += x2;
             acc += x3;
-            off += 4 * Qs;
-            off = off >= re ? off - span : off;
+            vo += 4 * Qs;
+            vo = vo >= re ? vo - span : vo;
         }
         const int r = len & 3;
         if (r) {
-            const char* p = lp + off;
+            const char* p = lds + vo + lane16;
             const f32x4 x0 = *reinterpret_cast<const f32x4*>(p);
             const f32x4 x1 = *reinterpret_cast<const f32x4*>(p + Qs);
             const f32x4 x2 = *reinterpret_cast<const f32x4*>(p + 2 * Qs);
@@ -592,93 +342,126 @@ __global__ __launch_bounds__(AX_THREADS) void k_agg_split(AggStream S, DevParams
     };
     const uint32_t mstep = AS_SEG * AX_MW * 4;
     const char* mbase = lds + meta_off + (uint32_t)w * AX_MW * 4;  // this wave's pixel column
+    // meta slot of chunk 12 b + u + d (b: the block, odd -> par): compile-time d and u
+    auto mslot = [&](bool par, int ud) -> uint32_t {
+        const int e = (ud % AX_MC + AX_MC) % AX_MC, o = (ud + AX_D) % AX_MC;
+        return (uint32_t)(par ? (o + AX_MC) % AX_MC : e) * mstep;
+    };
+    // the volume store of pass B / the single pass: byte offset from the slice base
+    const __amdgpu_buffer_rsrc_t rs_vol = make_rsrc(volq);
+    auto store = [&](uint32_t lo, uint32_t hi, const f32x4& acc) {
+        if (!vl) return;
+        if (BIG) {
+            const size_t o = ((size_t)hi << 32 | lo) >> 2;
+            st_stream(volq + o + 4 * lane, acc);
+        } else {
+            __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, acc), rs_vol, lane16, lo, 2);
+        }
+    };
 
     if (roleA) {
         // ---- A: staging ring, land, pass A ----------------------------------------------
         const int lanec = lane < Q ? lane : Q - 1;
-        const __amdgpu_buffer_rsrc_t rs_vol = make_rsrc(volq), rs_pk = make_rsrc(S.pk),
-                                     rs_rcp = make_rsrc(S.rcp);
+        const __amdgpu_buffer_rsrc_t rs_pk = make_rsrc(S.pk), rs_rcp = make_rsrc(S.rcp);
         const uint32_t voff = (uint32_t)lanec * 16;
-        const uint32_t es4 = (uint32_t)(es * 4), aes4 = (uint32_t)(aes * 4);
-        // the meta words are uniform; an opaque zero lane offset keeps them in VGPRs
-        // (uniform values would be moved to SGPRs right after the load: a wait per load)
-        uint32_t vzero;
-        asm volatile("v_mov_b32 %0, 0" : "=v"(vzero));
-        // issue position (chunk ci = s + AHEAD + AX_D at step s), advanced one chunk a step
-        int il = 0, icc = 0;
-        uint32_t iv = 0, ia = 0;  // byte offsets of line il: vol, descriptors (= reciprocals)
-        const float* ivp = volq;   // BIG: line il's first pixel
-        auto set_line = [&]() {
-            const int gl = g + il * G;
-            const int v = gl / S.nlv, line = gl - v * S.nlv;
-            if (BIG) ivp = volq + (size_t)v * vstride + (size_t)line * ls;
-            else iv = (uint32_t)(((size_t)v * vstride + (size_t)line * ls) * 4);
-            ia = (uint32_t)(2 * v * H * W + line * (int)als) * 4;  // per-view stride 2HW
+        // Chunks c0 .. c0 + AX_D - 1, lane k for chunk c0 + k: the volume byte offset of pixel
+        // w (64-bit), whether the pixel is inside the workgroup's stream, and its packed
+        // arms + window size and reciprocal (loaded here, used a block later).  (bl, bc):
+        // line / chunk-in-line of c0, advanced AX_D chunks a block (scalar, once a block).
+        struct Batch { uint32_t olo, ohi, valid, ma, my; };
+        int bl = 0, bc = 0;
+        auto batch = [&]() -> Batch {
+            int c = bc + (lane < AX_D ? lane : 0), l = bl;
+            while (c >= S.cpl) { c -= S.cpl; ++l; }
+            const bool past = l >= my_lines;
+            const int lc = past ? my_lines - 1 : l;  // past the end: re-read the last pixel
+            const int pos = past ? S.n - 1 : min(c * AS_SEG + w, S.n - 1);
+            const int gl = g + lc * G;
+            const int v = gl >= S.nlv ? 1 : 0, line = gl - v * S.nlv;
+            const size_t ob = ((size_t)v * vstride + (size_t)line * ls + (size_t)pos * es) * 4;
+            const uint32_t mo = ((uint32_t)(2 * v * H * W) + (uint32_t)line * als + (uint32_t)pos * aes) * 4;  // per-view stride 2HW
+            Batch B;
+            B.olo = (uint32_t)ob;
+            B.ohi = BIG ? (uint32_t)(ob >> 32) : 0u;
+            B.valid = (!past && c * AS_SEG + w < S.n) ? 1u : 0u;
+            B.ma = (uint32_t)__builtin_amdgcn_raw_buffer_load_b32(rs_pk, mo, 0, 0);
+            B.my = S.ws ? (uint32_t)__builtin_amdgcn_raw_buffer_load_b32(rs_rcp, mo, 0, 0) : 0u;
+            return B;
         };
-        set_line();
-        f32x4 rv[AX_D];
-        uint32_t rma[AX_D], rmy[AX_D];  // packed descriptor, RN(1/size) bits
-        auto issue = [&](int k) {  // chunk at (il, icc) -> slot k; past the end: re-read the last pixel
-            const bool past = il >= my_lines;
-            const uint32_t pos = past ? (uint32_t)(S.n - 1) : (uint32_t)min(icc * AS_SEG + w, S.n - 1);
-            if (BIG)
-                rv[k] = *reinterpret_cast<const f32x4*>(ivp + (size_t)pos * es + 4 * lanec);
-            else
-                rv[k] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rs_vol, voff, iv + pos * es4, 0));
-            rma[k] = (uint32_t)__builtin_amdgcn_raw_buffer_load_b32(rs_pk, vzero, ia + pos * aes4, 0);
-            rmy[k] = S.ws ? (uint32_t)__builtin_amdgcn_raw_buffer_load_b32(rs_rcp, vzero, ia + pos * aes4, 0) : vzero;
-            if (!past && ++icc == S.cpl) {
-                icc = 0;
-                ++il;
-                if (il < my_lines) set_line();
+        auto advance = [&](int k) {
+            bc += k;
+            while (bc >= S.cpl) { bc -= S.cpl; ++bl; }
+        };
+        // descriptors of batch Bt's chunks (chunk c0 + k in lane k, lanes < n) -> the meta
+        // ring; the chunks' ring slot index is (r0 + k) % AX_D, their meta slot (m0 + k) % AX_MC
+        auto finish = [&](const Batch& Bt, int r0, int m0, int n) {
+            if (lane < n) {
+                const int slot = ((r0 + lane) % AX_D) * AS_SEG + w;
+                const int lo = (int)(Bt.ma & 0xffu), hi = (int)((Bt.ma >> 8) & 0xffu);
+                int st = slot - lo;
+                st = st < 0 ? st + AS_RP1 : st;
+                const uint32_t len = Bt.valid ? (uint32_t)(lo + hi + 1) : 0u;
+                char* m = lds + meta_off + (uint32_t)(((m0 + lane) % AX_MC) * AS_SEG + w) * AX_MW * 4;
+                *reinterpret_cast<u32x4*>(m) = u32x4{r1_off + (uint32_t)st * Qs, len, Bt.my,
+                                                     __float_as_uint((float)(int)(Bt.ma >> 16))};
+                *reinterpret_cast<u32x2*>(m + 16) = u32x2{Bt.olo, Bt.ohi};
             }
         };
-        // pixel w of chunk c -> ring1; its raw descriptor (arms, window size, reciprocal)
-        // -> the meta ring (every lane writes the same 16 B: no exec branch)
-        auto land = [&](const f32x4& val, uint32_t ma, uint32_t my, int c) {
-            const int slot = (c % AS_RC1) * AS_SEG + w;
+        f32x4 rv[AX_D];
+        auto issue = [&](int k, const Batch& Bt, int i) {  // chunk of lane i of batch Bt -> slot k
+            const uint32_t lo = __builtin_amdgcn_readlane(Bt.olo, i);
+            if (BIG) {
+                const uint32_t hi = __builtin_amdgcn_readlane(Bt.ohi, i);
+                const size_t o = ((size_t)hi << 32 | lo) >> 2;
+                rv[k] = *reinterpret_cast<const f32x4*>(volq + o + 4 * lanec);
+            } else {
+                // single passes (the first and the last) load with the streaming policy (kNtLoad)
+                rv[k] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rs_vol, voff, lo, FUSED ? 0 : kNtLoad));
+            }
+        };
+        auto land = [&](const f32x4& val, int ci) {  // pixel w of a chunk -> ring1 slot index ci
+            const int slot = ci * AS_SEG + w;
             *reinterpret_cast<f32x4*>(lds + r1_off + (uint32_t)slot * Qs + voff) = val;
             if (slot < AX_MIR) *reinterpret_cast<f32x4*>(lds + r1_off + (uint32_t)(AS_RP1 + slot) * Qs + voff) = val;
-            *reinterpret_cast<u32x2*>(lds + meta_off + (uint32_t)((c % AX_MC) * AS_SEG + w) * AX_MW * 4) = u32x2{ma, my};
         };
         // prologue: chunks 0 .. AHEAD + AX_D - 1 in flight, chunks 0 .. AHEAD - 1 landed.
         // Slot of chunk c: (c - AHEAD) mod AX_D, so step s lands and refills slot s mod AX_D.
+        const Batch b0 = batch();  // chunks 0 .. AX_D - 1
         f32x4 pre[AS_AHEAD];
-        uint32_t pma[AS_AHEAD], pmy[AS_AHEAD];
 #pragma unroll
         for (int c = 0; c < AS_AHEAD; ++c) {
-            issue(0);
+            issue(0, b0, c);
             pre[c] = rv[0];
-            pma[c] = rma[0];
-            pmy[c] = rmy[0];
         }
+        advance(AS_AHEAD);
+        Batch prev = batch();  // chunks AHEAD .. AHEAD + AX_D - 1: land in block 0
 #pragma unroll
-        for (int k = 0; k < AX_D; ++k) issue(k);
+        for (int k = 0; k < AX_D; ++k) issue(k, prev, k);
+        advance(AX_D);
+        finish(b0, 0, 0, AS_AHEAD);
 #pragma unroll
-        for (int c = 0; c < AS_AHEAD; ++c) land(pre[c], pma[c], pmy[c], c);
-        int ca = 0, cc_a = 0;  // pass-A chunk s: position in its line (validity of pixel w)
-        // AX_D == ring chunks: every ring slot below is a compile-time function of u
-        u32x2 mA;
+        for (int c = 0; c < AS_AHEAD; ++c) land(pre[c], c % AX_D);
+        u32x4 mA;
         barrier();
-        mA = *reinterpret_cast<const u32x2*>(mbase);
+        mA = *reinterpret_cast<const u32x4*>(mbase);
         for (int b = 0; b < nblk; ++b) {
+            const bool par = b & 1;
+            const Batch cur = batch();  // chunks issued in this block (land in the next)
+            advance(AX_D);
+            // the descriptors of this block's landing chunks 12 b + AHEAD + k
+            finish(prev, AS_AHEAD, (par ? AX_D : 0) + AS_AHEAD, AX_D);
 #pragma unroll
             for (int u = 0; u < AX_D; ++u) {
-                const int s = b * AX_D + u;
                 // land chunk s + AHEAD from slot u, then refill the slot (chunk s + AHEAD + AX_D)
-                land(rv[u], rma[u], rmy[u], s + AS_AHEAD);
-                issue(u);
-                const uint32_t arm = __builtin_amdgcn_readfirstlane(mA.x);
-                const float a_y = __uint_as_float(__builtin_amdgcn_readfirstlane(mA.y));
-                const float a_b = (float)(int)(arm >> 16);
-                const int lo = (int)(arm & 0xffu), hi = (int)((arm >> 8) & 0xffu);
-                int st = u * AS_SEG + w - lo;  // ring1 slot of chunk s pixel w, minus the arm
-                st = st < 0 ? st + AS_RP1 : st;
-                const uint32_t a_off = r1_off + (uint32_t)st * Qs;
-                const int a_len = lo + hi + 1;
-                mA = *reinterpret_cast<const u32x2*>(mbase + ((u + 1) % AX_MC) * mstep);  // chunk s + 1 (landed)
+                land(rv[u], (u + AS_AHEAD) % AX_D);
+                issue(u, cur, u);
+                const uint32_t a_off = __builtin_amdgcn_readfirstlane(mA.x);
+                const int a_len = (int)__builtin_amdgcn_readfirstlane(mA.y);
+                const float a_y = __uint_as_float(__builtin_amdgcn_readfirstlane(mA.z));
+                const float a_b = __uint_as_float(__builtin_amdgcn_readfirstlane(mA.w));
+                mA = *reinterpret_cast<const u32x4*>(mbase + mslot(par, u + 1));  // chunk s + 1
                 const uint32_t r2w = r2_off + (uint32_t)(u * AS_SEG + w) * Qs;  // ring2 slot of chunk s
-                if (s < nch && cc_a * AS_SEG + w < S.n) {
+                if (a_len) {
                     f32x4 acc = window(a_off, a_len, r1_off, r1_end);
                     if (S.ws) acc = div_ws(acc, a_b, a_y);
                     if (vl) {
@@ -687,51 +470,41 @@ __global__ __launch_bounds__(AX_THREADS) void k_agg_split(AggStream S, DevParams
                             *reinterpret_cast<f32x4*>(lds + r2w + (uint32_t)AS_RP2 * Qs + lane16) = acc;
                     }
                 }
-                if (++cc_a == S.cpl) cc_a = 0;
-                (void)ca;
                 barrier();
             }
+            prev = cur;
         }
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // no load outlives the workgroup
         return;
     }
 
     // ---- B: pass B over ring2 (FUSED) or pass A's outputs out of ring2, stores ------------
-    struct Out {
-        int lidx, cc;
-        size_t off;
-    };
-    auto out_init = [&](Out& o) { o.lidx = 0; o.cc = 0; o.off = line_base(0) + (size_t)w * es; };
-    auto out_step = [&](Out& o) {
-        if (++o.cc == S.cpl) { o.cc = 0; ++o.lidx; if (o.lidx < my_lines) o.off = line_base(o.lidx) + (size_t)w * es; }
-        else o.off += (size_t)AS_SEG * es;
-    };
-    Out ob;
-    out_init(ob);
     constexpr int lag = FUSED ? AS_LAG : 1;
+    const uint32_t d21 = r2_off - r1_off;  // pass B's window: pass A's ring1 start, in ring2
     barrier();
-    uint32_t mB = *reinterpret_cast<const uint32_t*>(mbase + ((AX_D - lag) % AX_MC) * mstep);  // arms of chunk -lag
+    u32x2 mB = u32x2{0u, 0u}, mO = u32x2{0u, 0u};  // chunk -lag: never used (s < lag)
     for (int b = 0; b < nblk; ++b) {
+        const bool par = b & 1;
 #pragma unroll
         for (int u = 0; u < AX_D; ++u) {
             const int s = b * AX_D + u;
-            const int ub = (u - lag + 2 * AX_D) % AX_D;  // ring / meta chunk slot of chunk s - lag
-            const uint32_t arm = __builtin_amdgcn_readfirstlane(mB);
-            const int lo = (int)(arm & 0xffu), hi = (int)((arm >> 8) & 0xffu);
-            int st = ub * AS_SEG + w - lo;
-            st = st < 0 ? st + AS_RP2 : st;
-            const uint32_t b_off = r2_off + (uint32_t)st * Qs;
-            const int b_len = lo + hi + 1;
-            mB = *reinterpret_cast<const uint32_t*>(mbase + ((ub + 1) % AX_MC) * mstep);
+            const int ub = (u - lag + 2 * AX_D) % AX_D;  // ring chunk slot of chunk s - lag
+            const uint32_t b_off = __builtin_amdgcn_readfirstlane(mB.x) + d21;
+            const int b_len = (int)__builtin_amdgcn_readfirstlane(mB.y);
+            const uint32_t olo = __builtin_amdgcn_readfirstlane(mO.x);
+            const uint32_t ohi = BIG ? __builtin_amdgcn_readfirstlane(mO.y) : 0u;
+            const char* mn = mbase + mslot(par, u - lag + 1);  // chunk s - lag + 1
+            mB = *reinterpret_cast<const u32x2*>(mn);
+            mO = *reinterpret_cast<const u32x2*>(mn + 16);
             const uint32_t r2r = r2_off + (uint32_t)(ub * AS_SEG + w) * Qs;  // single: chunk s - 1
-            const int sb = s - lag;
-            if (sb >= 0 && sb < nch) {
-                if (ob.cc * AS_SEG + w < S.n) {
-                    const f32x4 acc = FUSED ? window(b_off, b_len, r2_off, r2_end)
-                                            : *reinterpret_cast<const f32x4*>(lds + r2r + lane16);
-                    if (vl) st_stream(volq + ob.off + 4 * lane, acc);
-                }
-                out_step(ob);
+            if (s >= lag && b_len) {
+                const f32x4 acc = FUSED ? window(b_off, b_len, r2_off, r2_end)
+                                        : *reinterpret_cast<const f32x4*>(lds + r2r + lane16);
+#ifdef TSM_EXP_AGG_NOSTORE  // timing probe: B waves compute but do not store
+                if (acc.x == -1.f) store(olo, ohi, acc);
+#else
+                store(olo, ohi, acc);
+#endif
             }
             barrier();
         }
@@ -786,13 +559,9 @@ __global__ __launch_bounds__(AL_THREADS) void k_agg_wholeline(float* __restrict_
 // ---------------------------------------------------------------------------
 // launchers
 // ---------------------------------------------------------------------------
-static size_t agg_stream_lds(const DevParams& P, bool fused) {
-    const int Q = P.Lp / 4;
-    return ((size_t)AS_RP1 + AX_MIR + (fused ? AS_RP2 + AX_MIR : 0)) * Q * 16 + (size_t)AS_MC * AS_SEG * AS_MW * 4;
-}
 // LDS of the split streamer for a slice of qs label vectors
 static size_t agg_split_lds(int qs) {
-    return ((size_t)AS_RP1 + AS_RP2 + 2 * AX_MIR) * qs * 16 + (size_t)AX_MC * AS_SEG * AX_MW * 4;
+    return ((size_t)AS_RP1 + AS_RP2 + 2 * AX_MIR) * qs * 16 + (size_t)AX_MC * AS_SEG * AX_MW * 4;  // rings + meta
 }
 constexpr size_t kLdsBytes = 160 * 1024;
 
@@ -846,34 +615,20 @@ int launch_aggregation_pass(float* vol, const uint32_t* arms, const int32_t* ws,
     S.nl = 2 * S.nlv;
     const int ncu = P.ncu;
     const int G = S.nl < ncu ? S.nl : ncu;
-    // fused pass pairs: the role-split streamer (v6); single passes: v5 where its rings fit
-    // (v6 for single passes too measured 1 % fewer pairs/s: round 3, same box)
-    const bool v5_fits = !fused && Q <= 64 && !big && agg_stream_lds(P, false) <= kLdsBytes;
-    if (!v5_fits) {
-        const size_t slds = agg_split_lds(S.qn0);
-        const dim3 sgrid(G, nslice, P.npairs);
-        if (fused) {
-            if (big) launch_split_t<true, 0, true>(S, P, sgrid, slds, st);
-            else if (Q == 49 && nslice == 1) launch_split_t<true, 49, false>(S, P, sgrid, slds, st);
-            else launch_split_t<true, 0, false>(S, P, sgrid, slds, st);
-        } else {
-            if (big) launch_split_t<false, 0, true>(S, P, sgrid, slds, st);
-            else if (Q == 49 && nslice == 1) launch_split_t<false, 49, false>(S, P, sgrid, slds, st);
-            else launch_split_t<false, 0, false>(S, P, sgrid, slds, st);
-        }
-        trace_point(fused ? "k_agg_split<fused>" : "k_agg_split", st);
-        return 0;
-    }
-    const size_t lds = agg_stream_lds(P, false);
-    const dim3 grid(G, 1, P.npairs), block(AS_THREADS);
-    if (Q == 49) {
-        ensure_lds_limit((const void*)k_agg_stream<false, 49>, kLdsBytes);
-        hipLaunchKernelGGL((k_agg_stream<false, 49>), grid, block, lds, st, S, P);
+    // every pass through the role-split streamer (round 4, same box: 409 against 406.5
+    // pairs/s with the single passes on the former loader/summer streamer)
+    const size_t slds = agg_split_lds(S.qn0);
+    const dim3 sgrid(G, nslice, P.npairs);
+    if (fused) {
+        if (big) launch_split_t<true, 0, true>(S, P, sgrid, slds, st);
+        else if (Q == 49 && nslice == 1) launch_split_t<true, 49, false>(S, P, sgrid, slds, st);
+        else launch_split_t<true, 0, false>(S, P, sgrid, slds, st);
     } else {
-        ensure_lds_limit((const void*)k_agg_stream<false, 0>, kLdsBytes);
-        hipLaunchKernelGGL((k_agg_stream<false, 0>), grid, block, lds, st, S, P);
+        if (big) launch_split_t<false, 0, true>(S, P, sgrid, slds, st);
+        else if (Q == 49 && nslice == 1) launch_split_t<false, 49, false>(S, P, sgrid, slds, st);
+        else launch_split_t<false, 0, false>(S, P, sgrid, slds, st);
     }
-    trace_point("k_agg_stream", st);
+    trace_point(fused ? "k_agg_split<fused>" : "k_agg_split", st);
     return 0;
 }
 

@@ -11,7 +11,7 @@ for set in "SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_AC
            "SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_VALU_MFMA_BUSY_CYCLES SQ_ACTIVE_INST_MISC" \
            "GRBM_GUI_ACTIVE GRBM_COUNT"; do
   i=$((i+1))
-  timeout -s KILL 120 rocprofv3 --pmc $set --kernel-include-regex "$RX" --output-format csv -d gpurun_out/pk_$i -o run -- python3 bench.py --steps 1 --warmup 1 --no-cpu-baseline --no-ops --batch 4 --concurrency 2 > gpurun_out/pk_$i.log 2>&1
-  rc=$?; echo "pass $i rc=$rc"; [ $rc -ne 0 ] && { tail -5 gpurun_out/pk_$i.log; exit $rc; }
+  timeout -s KILL 120 rocprofv3 --pmc $set --kernel-include-regex "$RX" --output-format csv -d gpurun_out/pk_${TAG:-x}_$i -o run -- python3 bench.py --steps 1 --warmup 1 --no-cpu-baseline --no-ops --no-configs --batch ${PMC_BATCH:-4} --concurrency ${PMC_CONC:-2} > gpurun_out/pk_${TAG:-x}_$i.log 2>&1
+  rc=$?; echo "pass $i rc=$rc"; [ $rc -ne 0 ] && { tail -5 gpurun_out/pk_${TAG:-x}_$i.log; exit $rc; }
 done
-python3 tools/pmc_sum.py gpurun_out/pk_*/run_counter_collection.csv
+python3 tools/pmc_sum.py gpurun_out/pk_${TAG:-x}_*/run_counter_collection.csv
