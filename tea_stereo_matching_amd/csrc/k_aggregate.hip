@@ -416,7 +416,11 @@ __global__ __launch_bounds__(AX_THREADS) void k_agg_split(AggStream S, DevParams
                 rv[k] = *reinterpret_cast<const f32x4*>(volq + o + 4 * lanec);
             } else {
                 // single passes (the first and the last) load with the streaming policy (kNtLoad)
+#ifdef TSM_EXP_AGG_NOLOAD  // timing probe: every A wave re-reads one L2-resident vector
+                rv[k] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rs_vol, voff, lo & 0xffffu, 0));
+#else
                 rv[k] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rs_vol, voff, lo, FUSED ? 0 : kNtLoad));
+#endif
             }
         };
         auto land = [&](const f32x4& val, int ci) {  // pixel w of a chunk -> ring1 slot index ci
@@ -462,7 +466,11 @@ __global__ __launch_bounds__(AX_THREADS) void k_agg_split(AggStream S, DevParams
                 mA = *reinterpret_cast<const u32x4*>(mbase + mslot(par, u + 1));  // chunk s + 1
                 const uint32_t r2w = r2_off + (uint32_t)(u * AS_SEG + w) * Qs;  // ring2 slot of chunk s
                 if (a_len) {
+#ifdef TSM_EXP_AGG_WIN1  // timing probe: one-pixel windows in pass A and pass B
+                    f32x4 acc = window(a_off, 1, r1_off, r1_end);
+#else
                     f32x4 acc = window(a_off, a_len, r1_off, r1_end);
+#endif
                     if (S.ws) acc = div_ws(acc, a_b, a_y);
                     if (vl) {
                         *reinterpret_cast<f32x4*>(lds + r2w + lane16) = acc;
@@ -498,7 +506,11 @@ __global__ __launch_bounds__(AX_THREADS) void k_agg_split(AggStream S, DevParams
             mO = *reinterpret_cast<const u32x2*>(mn + 16);
             const uint32_t r2r = r2_off + (uint32_t)(ub * AS_SEG + w) * Qs;  // single: chunk s - 1
             if (s >= lag && b_len) {
+#ifdef TSM_EXP_AGG_WIN1
+                const f32x4 acc = FUSED ? window(b_off, 1, r2_off, r2_end)
+#else
                 const f32x4 acc = FUSED ? window(b_off, b_len, r2_off, r2_end)
+#endif
                                         : *reinterpret_cast<const f32x4*>(lds + r2r + lane16);
 #ifdef TSM_EXP_AGG_NOSTORE  // timing probe: B waves compute but do not store
                 if (acc.x == -1.f) store(olo, ohi, acc);
