@@ -295,7 +295,8 @@ __global__ __launch_bounds__(CW_THREADS) __attribute__((amdgpu_waves_per_eu(E ==
     for (int i = threadIdx.x; i < 2 * CW_LUTB; i += CW_THREADS)
         sB[i] = i < 188 ? lutB[i] : (i >= CW_LUTB ? -__int_as_float(0x7f800000) : 0.f);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // ring prologue landed (LDS-DMA)
-    __syncthreads();  // tables ready: the kernel's only barrier
+    __syncthreads();  // tables ready: the kernel's only barrier (waiting here costs nothing
+                      // measurable: a probe without it ran 200.3 against 200.6 us, round 4)
     if (!active) return;
 
     // warm-up: label k = kb + E*lane + e holds the varying record at x = j0 - k (view 0)
