@@ -12,7 +12,7 @@ LIB      := $(LIBDIR)/libtsm_adcensus.so
 HIPFLAGS := --offload-arch=$(ARCH) -O3 -std=c++20 -fPIC -ffp-contract=off \
             -fhip-fp32-correctly-rounded-divide-sqrt -Wall -Wno-unused-result -Wno-unused-value -Iinclude
 HIP_SRCS := k_cost k_aggregate k_scanline k_refine k_stereo_ops
-CPP_SRCS := engine stereo_ops stereo_ops_api
+CPP_SRCS := engine stereo_ops
 OBJS     := $(addprefix $(OBJ)/,$(addsuffix .o,$(HIP_SRCS) $(CPP_SRCS)))
 HDRS     := $(SRC)/copy_pool.h $(SRC)/tsm_device.h $(SRC)/tsm_launch.h include/tsm_adcensus.h include/stereo.h include/tsm_stereo_ops.h
 

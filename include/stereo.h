@@ -13,6 +13,7 @@
 // ImageView / DisparityMap form is then an overload (and the virtual without OpenCV).
 // StereoMatching and ADCensus are header-only over the C ABI (link libtsm_adcensus.so).
 #pragma once
+#include <algorithm>
 #include <array>
 #include <cstddef>
 #include <cstdint>
@@ -22,6 +23,7 @@
 #include <vector>
 
 #include "tsm_adcensus.h"
+#include "tsm_stereo_ops.h"
 
 #if __has_include(<opencv2/core/mat.hpp>)
 #include <opencv2/core/mat.hpp>
@@ -234,8 +236,17 @@ private:
 };
 
 // ---- the calls either side of the matcher, gfx950 kernels through
-// include/tsm_stereo_ops.h.  Device failures throw std::runtime_error; the reference's
-// "log and return" cases (empty inputs, maps not loaded) return without output.
+// include/tsm_stereo_ops.h, header-only like the matcher.  Device failures throw
+// std::runtime_error; the reference's "log and return" cases (empty inputs, maps not
+// loaded) return without output.  With OpenCV the reference's cv::Mat signatures
+// (reference include/stereo.h:194-296) are declared as well, and JETColorMap() returns the
+// reference's 1 x 256 CV_8UC3 cv::Mat; JETColorMapTable() returns the light table either way.
+
+namespace detail {
+inline void ops_check(int rc, const char* what) {
+    if (rc != TSM_OK) throw std::runtime_error(std::string(what) + " failed (status " + std::to_string(rc) + ")");
+}
+}  // namespace detail
 
 /** Owning BGR u8 image (CV_8UC3 equivalent, dense rows). */
 struct ColorImage {
@@ -257,30 +268,90 @@ struct PointImage {
 /** A colour table as stereo::JETColorMap returns it (1 x 256 CV_8UC3): lut[3*i + c], BGR. */
 using ColorMapTable = std::array<std::uint8_t, 768>;
 
-/** stereo.cpp:75-92 */
-ColorMapTable JETColorMap();
+/** stereo.cpp:75-92, as a light table */
+inline ColorMapTable JETColorMapTable() {
+    ColorMapTable t{};
+    detail::ops_check(tsm_jet_colormap(t.data()), "JETColorMap");
+    return t;
+}
+
+namespace detail {
+inline void color_map(const DisparityMap& src, ColorImage& dst, int use_range, float mn, float mx,
+                      const ColorMapTable& lut) {
+    if (src.empty()) return;
+    dst.rows = src.rows;
+    dst.cols = src.cols;
+    dst.data.assign((std::size_t)src.rows * src.cols * 3, 0);
+    ops_check(tsm_apply_colormap(src.data.data(), src.rows, src.cols, (std::size_t)src.cols * 4, lut.data(),
+                                 use_range, mn, mx, dst.data.data(), (std::size_t)src.cols * 3),
+              "applyColorMap");
+}
+}  // namespace detail
+
 /** stereo.cpp:94-118: range from the pixels >= 0 and not inf; pixels < 0 black. */
-void applyColorMap(const DisparityMap& src, ColorImage& dst, const ColorMapTable& colorMap);
+inline void applyColorMap(const DisparityMap& src, ColorImage& dst, const ColorMapTable& colorMap) {
+    detail::color_map(src, dst, 0, 0.f, 0.f, colorMap);
+}
 /** stereo.cpp:120-134: pixels outside [minVal, maxVal] black. */
-void applyColorMap(const DisparityMap& src, ColorImage& dst, float minVal, float maxVal,
-                   const ColorMapTable& colorMap);
+inline void applyColorMap(const DisparityMap& src, ColorImage& dst, float minVal, float maxVal,
+                          const ColorMapTable& colorMap) {
+    detail::color_map(src, dst, 1, minVal, maxVal, colorMap);
+}
 /** stereo.cpp:136-148: depth = f*b / d (0 where d < 0 or inf); `depth` is a fp32 map. */
-void reprojectToDepth(const DisparityMap& disparity, float focalLength, float baseline, DisparityMap& depth);
+inline void reprojectToDepth(const DisparityMap& d, float focalLength, float baseline, DisparityMap& depth) {
+    if (d.empty()) return;
+    depth.rows = d.rows;
+    depth.cols = d.cols;
+    depth.data.assign(d.data.size(), 0.f);
+    detail::ops_check(tsm_reproject_to_depth(d.data.data(), d.rows, d.cols, (std::size_t)d.cols * 4, focalLength,
+                                             baseline, depth.data.data(), (std::size_t)d.cols * 4),
+                      "reprojectToDepth");
+}
 /** stereo.cpp:150-169 */
-void reprojectTo3D(const DisparityMap& disparity, float focalLength, float baseline, float cx, float cy,
-                   PointImage& XYZPoints);
+inline void reprojectTo3D(const DisparityMap& d, float focalLength, float baseline, float cx, float cy,
+                          PointImage& xyz) {
+    if (d.empty()) return;
+    xyz.rows = d.rows;
+    xyz.cols = d.cols;
+    xyz.data.assign(d.data.size() * 3, 0.f);
+    detail::ops_check(tsm_reproject_to_3d(d.data.data(), d.rows, d.cols, (std::size_t)d.cols * 4, focalLength,
+                                          baseline, cx, cy, xyz.data.data(), (std::size_t)d.cols * 12),
+                      "reprojectTo3D");
+}
 /** stereo.cpp:171-202: Q is the 4x4 reprojection matrix, row-major (CV_64F). */
-void reprojectTo3D(const DisparityMap& disparity, const std::array<double, 16>& Q, PointImage& XYZPoints);
+inline void reprojectTo3D(const DisparityMap& d, const std::array<double, 16>& Q, PointImage& xyz) {
+    if (d.empty()) return;
+    xyz.rows = d.rows;
+    xyz.cols = d.cols;
+    xyz.data.assign(d.data.size() * 3, 0.f);
+    detail::ops_check(tsm_reproject_to_3d_q(d.data.data(), d.rows, d.cols, (std::size_t)d.cols * 4, Q.data(),
+                                            xyz.data.data(), (std::size_t)d.cols * 12),
+                      "reprojectTo3D");
+}
 /** stereo.cpp:250-278 (RGBImage is BGR-ordered, as the reference's cv::Mat) */
-void writePointCloudToPCD(const ImageView& RGBImage, const PointImage& XYZPoints, const std::string& pcdPath);
+inline void writePointCloudToPCD(const ImageView& img, const PointImage& xyz, const std::string& path) {
+    if (img.empty() || xyz.empty() || path.empty()) return;  // "Empty input." (stereo.cpp:252-256)
+    detail::ops_check(tsm_write_point_cloud_pcd(img.data, img.step, xyz.data.data(), (std::size_t)xyz.cols * 12,
+                                                xyz.rows, xyz.cols, path.c_str()),
+                      "writePointCloudToPCD");
+}
 /** stereo.cpp:328-356 */
-void writePointCloudToPLY(const ImageView& RGBImage, const PointImage& XYZPoints, const std::string& plyPath);
+inline void writePointCloudToPLY(const ImageView& img, const PointImage& xyz, const std::string& path) {
+    if (img.empty() || xyz.empty() || path.empty()) return;
+    detail::ops_check(tsm_write_point_cloud_ply(img.data, img.step, xyz.data.data(), (std::size_t)xyz.cols * 12,
+                                                xyz.rows, xyz.cols, path.c_str()),
+                      "writePointCloudToPLY");
+}
 
 /** cv::Size */
 struct Size {
     int width = 0;
     int height = 0;
 };
+
+#ifndef TSM_HAVE_OPENCV
+/** stereo.cpp:75-92 */
+inline ColorMapTable JETColorMap() { return JETColorMapTable(); }
 
 /** stereo::EpipolarRectifyMap (stereo_utils.cpp:88-174), the remap pairs in the form
  *  initUndistortRectifyMap(..., CV_16SC2, ...) makes them (stereo_utils.cpp:164-167):
@@ -293,26 +364,244 @@ struct EpipolarRectifyMap {
     std::vector<std::uint16_t> map01, map11;  // rows * cols
     bool empty() const { return map00.empty() || map01.empty() || map10.empty() || map11.empty(); }
 };
+#else
+/** stereo.cpp:75-92: the reference's 1 x 256 CV_8UC3 table */
+inline cv::Mat JETColorMap() {
+    cv::Mat m(1, 256, CV_8UC3);
+    detail::ops_check(tsm_jet_colormap(m.ptr<std::uint8_t>(0)), "JETColorMap");
+    return m;
+}
+
+namespace detail {
+inline void need(bool ok, const char* what) {
+    if (!ok) throw std::runtime_error(what);
+}
+inline ColorMapTable table_of(const cv::Mat& colorMap) {
+    need(colorMap.type() == CV_8UC3 && colorMap.rows * colorMap.cols >= 256, "colorMap must be 256 CV_8UC3 entries");
+    ColorMapTable t{};
+    for (int i = 0; i < 256; ++i) {  // row-major over the table (1 x 256 or 256 x 1)
+        const std::uint8_t* e = colorMap.ptr<std::uint8_t>(i / colorMap.cols) + (std::size_t)(i % colorMap.cols) * 3;
+        t[3 * i] = e[0];
+        t[3 * i + 1] = e[1];
+        t[3 * i + 2] = e[2];
+    }
+    return t;
+}
+inline void color_map(const cv::Mat& src, cv::Mat& dst, int use_range, float mn, float mx, const cv::Mat& colorMap) {
+    if (src.empty()) { dst = cv::Mat(); return; }
+    need(src.type() == CV_32FC1, "applyColorMap: src must be CV_32FC1");
+    const ColorMapTable lut = table_of(colorMap);
+    cv::Mat out(src.rows, src.cols, CV_8UC3);  // dst = cv::Mat::zeros(src.size(), CV_8UC3) (:106)
+    ops_check(tsm_apply_colormap(src.ptr<float>(0), src.rows, src.cols, (std::size_t)src.step[0], lut.data(), use_range,
+                                 mn, mx, out.ptr<std::uint8_t>(0), (std::size_t)out.step[0]),
+              "applyColorMap");
+    dst = out;
+}
+}  // namespace detail
+
+/** stereo.cpp:94-118 */
+inline void applyColorMap(const cv::Mat& src, cv::Mat& dst, const cv::Mat& colorMap) {
+    detail::color_map(src, dst, 0, 0.f, 0.f, colorMap);
+}
+/** stereo.cpp:120-134 */
+inline void applyColorMap(const cv::Mat& src, cv::Mat& dst, float minVal, float maxVal, const cv::Mat& colorMap) {
+    detail::color_map(src, dst, 1, minVal, maxVal, colorMap);
+}
+/** stereo.cpp:136-148 */
+inline void reprojectToDepth(const cv::Mat& disparity, float focalLength, float baseline, cv::Mat& depth) {
+    if (disparity.empty()) { depth = cv::Mat(); return; }
+    detail::need(disparity.type() == CV_32FC1, "reprojectToDepth: disparity must be CV_32FC1");
+    cv::Mat out(disparity.rows, disparity.cols, CV_32FC1);
+    detail::ops_check(tsm_reproject_to_depth(disparity.ptr<float>(0), disparity.rows, disparity.cols,
+                                             (std::size_t)disparity.step[0], focalLength, baseline,
+                                             out.ptr<float>(0), (std::size_t)out.step[0]),
+                      "reprojectToDepth");
+    depth = out;
+}
+/** stereo.cpp:150-169 */
+inline void reprojectTo3D(const cv::Mat& disparity, float focalLength, float baseline, float cx, float cy,
+                          cv::Mat& XYZPoints) {
+    if (disparity.empty()) { XYZPoints = cv::Mat(); return; }
+    detail::need(disparity.type() == CV_32FC1, "reprojectTo3D: disparity must be CV_32FC1");
+    cv::Mat out(disparity.rows, disparity.cols, CV_32FC3);
+    detail::ops_check(tsm_reproject_to_3d(disparity.ptr<float>(0), disparity.rows, disparity.cols,
+                                          (std::size_t)disparity.step[0], focalLength, baseline, cx, cy,
+                                          out.ptr<float>(0), (std::size_t)out.step[0]),
+                      "reprojectTo3D");
+    XYZPoints = out;
+}
+/** stereo.cpp:171-202: Q 4 x 4, CV_32FC1 or CV_64FC1 */
+inline void reprojectTo3D(const cv::Mat& disparity, const cv::Mat& Q, cv::Mat& XYZPoints) {
+    if (disparity.empty()) { XYZPoints = cv::Mat(); return; }
+    detail::need(disparity.type() == CV_32FC1, "reprojectTo3D: disparity must be CV_32FC1");
+    detail::need(Q.rows == 4 && Q.cols == 4 && (Q.type() == CV_64FC1 || Q.type() == CV_32FC1),
+                 "reprojectTo3D: Q must be 4 x 4 CV_32FC1 / CV_64FC1");
+    double q[16];
+    for (int r = 0; r < 4; ++r)
+        for (int c = 0; c < 4; ++c)
+            q[4 * r + c] = Q.type() == CV_64FC1 ? Q.ptr<double>(r)[c] : (double)Q.ptr<float>(r)[c];
+    cv::Mat out(disparity.rows, disparity.cols, CV_32FC3);
+    detail::ops_check(tsm_reproject_to_3d_q(disparity.ptr<float>(0), disparity.rows, disparity.cols,
+                                            (std::size_t)disparity.step[0], q, out.ptr<float>(0),
+                                            (std::size_t)out.step[0]),
+                      "reprojectTo3D");
+    XYZPoints = out;
+}
+/** stereo.cpp:250-278 */
+inline void writePointCloudToPCD(const cv::Mat& RGBImage, const cv::Mat& XYZPoints, const std::string& pcdPath) {
+    if (RGBImage.empty() || XYZPoints.empty() || pcdPath.empty()) return;  // "Empty input." (:252-256)
+    detail::need(RGBImage.type() == CV_8UC3 && XYZPoints.type() == CV_32FC3 && RGBImage.size() == XYZPoints.size(),
+                 "writePointCloudToPCD: CV_8UC3 image and CV_32FC3 points of one size");
+    detail::ops_check(tsm_write_point_cloud_pcd(RGBImage.ptr<std::uint8_t>(0), (std::size_t)RGBImage.step[0],
+                                                XYZPoints.ptr<float>(0), (std::size_t)XYZPoints.step[0],
+                                                XYZPoints.rows, XYZPoints.cols, pcdPath.c_str()),
+                      "writePointCloudToPCD");
+}
+/** stereo.cpp:328-356 */
+inline void writePointCloudToPLY(const cv::Mat& RGBImage, const cv::Mat& XYZPoints, const std::string& plyPath) {
+    if (RGBImage.empty() || XYZPoints.empty() || plyPath.empty()) return;
+    detail::need(RGBImage.type() == CV_8UC3 && XYZPoints.type() == CV_32FC3 && RGBImage.size() == XYZPoints.size(),
+                 "writePointCloudToPLY: CV_8UC3 image and CV_32FC3 points of one size");
+    detail::ops_check(tsm_write_point_cloud_ply(RGBImage.ptr<std::uint8_t>(0), (std::size_t)RGBImage.step[0],
+                                                XYZPoints.ptr<float>(0), (std::size_t)XYZPoints.step[0],
+                                                XYZPoints.rows, XYZPoints.cols, plyPath.c_str()),
+                      "writePointCloudToPLY");
+}
+
+/** stereo_utils.h:109-148: the rectification maps as initUndistortRectifyMap makes them
+ *  (map00 / map10 CV_16SC2 + map01 / map11 CV_16UC1, or CV_32FC1 x / y map pairs).  The
+ *  YAML loader and compute() (calibration) are out of scope. */
+class EpipolarRectifyMap {
+public:
+    cv::Mat R1, R2, P1, P2;
+    cv::Mat map00, map01, map10, map11;
+    EpipolarRectifyMap() = default;
+    EpipolarRectifyMap(const cv::Mat& R1_, const cv::Mat& R2_, const cv::Mat& P1_, const cv::Mat& P2_,
+                       const cv::Mat& m00, const cv::Mat& m01, const cv::Mat& m10, const cv::Mat& m11)
+        : R1(R1_), R2(R2_), P1(P1_), P2(P2_), map00(m00), map01(m01), map10(m10), map11(m11) {}
+    bool empty() const { return map00.empty() || map01.empty() || map10.empty() || map11.empty(); }
+};
+#endif
 
 /** stereo.h:254-296 / EpipolarRectify.cpp -- INTER_LINEAR remap of both views. */
 class EpipolarRectify {
 public:
-    EpipolarRectify();
-    EpipolarRectify(const EpipolarRectifyMap& rectifyMap, const Size& imgsz);
-    ~EpipolarRectify();
+    EpipolarRectify() = default;
+#ifdef TSM_HAVE_OPENCV
+    EpipolarRectify(const EpipolarRectifyMap& rectifyMap, const cv::Size& imgsz) {
+        loadEpipolarRectifyMap(rectifyMap, imgsz);
+    }
     /** Throws std::runtime_error("stereo params is empty, please load it first") on empty maps. */
-    void loadEpipolarRectifyMap(const EpipolarRectifyMap& rectifyMap, const Size& imgsz);
+    void loadEpipolarRectifyMap(const EpipolarRectifyMap& rectifyMap, const cv::Size& imgsz) {
+        if (rectifyMap.empty()) throw std::runtime_error("stereo params is empty, please load it first");
+        m_rectifyMap = rectifyMap;
+        m_imgsz = Size{imgsz.width, imgsz.height};
+    }
     /** Side-by-side stereo image in, side-by-side rectified image out (:46-64). */
-    void rectify(const ImageView& stereoImage, ColorImage& rectifiedStereoImage);
+    void rectify(const cv::Mat& stereoImage, cv::Mat& rectifiedStereoImage) {
+        cv::Mat l, r;
+        rectify(stereoImage, l, r);
+        if (l.empty()) return;
+        cv::Mat out(l.rows, l.cols + r.cols, l.type());  // cv::hconcat
+        const std::size_t lb = (std::size_t)l.cols * l.elemSize(), rb = (std::size_t)r.cols * r.elemSize();
+        for (int y = 0; y < out.rows; ++y) {
+            std::copy_n(l.ptr<std::uint8_t>(y), lb, out.ptr<std::uint8_t>(y));
+            std::copy_n(r.ptr<std::uint8_t>(y), rb, out.ptr<std::uint8_t>(y) + lb);
+        }
+        rectifiedStereoImage = out;
+    }
     /** Side-by-side stereo image in, both rectified views out (:66-82). */
-    void rectify(const ImageView& stereoImage, ColorImage& rectifyLeftImage, ColorImage& rectifiedRightImage);
+    void rectify(const cv::Mat& stereoImage, cv::Mat& rectifyLeftImage, cv::Mat& rectifiedRightImage) {
+        if (m_rectifyMap.empty() || stereoImage.empty()) return;  // logged and returned (:68-77)
+        const int w = m_imgsz.width, h = m_imgsz.height;
+        const cv::Mat left = stereoImage(cv::Rect(0, 0, w, h)), right = stereoImage(cv::Rect(w, 0, w, h));
+        rectify(left, right, rectifyLeftImage, rectifiedRightImage);
+    }
     /** Both views in, both rectified views out (:84-101). */
-    void rectify(const ImageView& leftImage, const ImageView& rightImage, ColorImage& rectifyLeftImage,
-                 ColorImage& rectifiedRightImage);
+    void rectify(const cv::Mat& leftImage, const cv::Mat& rightImage, cv::Mat& rectifyLeftImage,
+                 cv::Mat& rectifiedRightImage) {
+        if (m_rectifyMap.empty() || leftImage.empty() || rightImage.empty()) return;  // :89-98
+        rectifyLeftImage = remap_mat(leftImage, m_rectifyMap.map00, m_rectifyMap.map01);
+        rectifiedRightImage = remap_mat(rightImage, m_rectifyMap.map10, m_rectifyMap.map11);
+    }
+#endif
+    EpipolarRectify(const EpipolarRectifyMap& rectifyMap, const Size& imgsz) { loadEpipolarRectifyMap(rectifyMap, imgsz); }
+    /** Throws std::runtime_error("stereo params is empty, please load it first") on empty maps. */
+    void loadEpipolarRectifyMap(const EpipolarRectifyMap& rectifyMap, const Size& imgsz) {
+        if (rectifyMap.empty()) throw std::runtime_error("stereo params is empty, please load it first");
+        m_rectifyMap = rectifyMap;
+        m_imgsz = imgsz;
+    }
+#ifndef TSM_HAVE_OPENCV
+    /** Side-by-side stereo image in, side-by-side rectified image out (:46-64). */
+    void rectify(const ImageView& stereoImage, ColorImage& out) {
+        ColorImage l, r;
+        rectify(stereoImage, l, r);
+        if (l.empty()) return;
+        out.rows = l.rows;
+        out.cols = l.cols + r.cols;
+        out.data.resize((std::size_t)out.rows * out.cols * 3);
+        for (int y = 0; y < out.rows; ++y) {  // cv::hconcat
+            std::uint8_t* o = out.data.data() + (std::size_t)y * out.cols * 3;
+            std::copy_n(l.data.data() + (std::size_t)y * l.cols * 3, (std::size_t)l.cols * 3, o);
+            std::copy_n(r.data.data() + (std::size_t)y * r.cols * 3, (std::size_t)r.cols * 3, o + (std::size_t)l.cols * 3);
+        }
+    }
+    /** Side-by-side stereo image in, both rectified views out (:66-82). */
+    void rectify(const ImageView& stereoImage, ColorImage& outL, ColorImage& outR) {
+        if (m_rectifyMap.empty() || stereoImage.empty()) return;  // logged and returned (:68-77)
+        const int w = m_imgsz.width, h = m_imgsz.height;
+        const ImageView left{stereoImage.data, h, w, stereoImage.step};
+        const ImageView right{stereoImage.data + (std::size_t)w * 3, h, w, stereoImage.step};
+        rectify(left, right, outL, outR);
+    }
+    /** Both views in, both rectified views out (:84-101). */
+    void rectify(const ImageView& leftImage, const ImageView& rightImage, ColorImage& outL, ColorImage& outR) {
+        if (m_rectifyMap.empty() || leftImage.empty() || rightImage.empty()) return;  // :89-98
+        const EpipolarRectifyMap& m = m_rectifyMap;
+        remap_view(leftImage, m.map00, m.map01, m.rows, m.cols, outL);
+        remap_view(rightImage, m.map10, m.map11, m.rows, m.cols, outR);
+    }
+#endif
 
 private:
     EpipolarRectifyMap m_rectifyMap;
     Size m_imgsz;
+#ifdef TSM_HAVE_OPENCV
+    /** cv::remap(src, dst, map1, map2, INTER_LINEAR) with BORDER_CONSTANT 0 (:99-100) */
+    static cv::Mat remap_mat(const cv::Mat& src, const cv::Mat& map1, const cv::Mat& map2) {
+        const int C = src.channels();
+        detail::need((src.type() & 7) == CV_8U && (C == 1 || C == 3 || C == 4), "rectify: 8-bit images of 1, 3 or 4 channels");
+        detail::need(map1.size() == map2.size(), "rectify: map sizes differ");
+        cv::Mat out(map1.rows, map1.cols, src.type());
+        int rc;
+        if (map1.type() == CV_16SC2 && (map2.type() == CV_16UC1 || map2.type() == CV_16SC1)) {
+            rc = tsm_remap_linear_fixed(src.ptr<std::uint8_t>(0), src.rows, src.cols, (std::size_t)src.step[0], C,
+                                        map1.ptr<std::int16_t>(0), (std::size_t)map1.step[0],
+                                        map2.ptr<std::uint16_t>(0), (std::size_t)map2.step[0], map1.rows, map1.cols,
+                                        out.ptr<std::uint8_t>(0), (std::size_t)out.step[0]);
+        } else {
+            detail::need(map1.type() == CV_32FC1 && map2.type() == CV_32FC1 && map1.step[0] == map2.step[0],
+                         "rectify: maps must be CV_16SC2 + CV_16UC1 or two CV_32FC1 of one step");
+            rc = tsm_remap_linear_float(src.ptr<std::uint8_t>(0), src.rows, src.cols, (std::size_t)src.step[0], C,
+                                        map1.ptr<float>(0), map2.ptr<float>(0), (std::size_t)map1.step[0],
+                                        map1.rows, map1.cols, out.ptr<std::uint8_t>(0), (std::size_t)out.step[0]);
+        }
+        detail::ops_check(rc, "rectify");
+        return out;
+    }
+#else
+    static void remap_view(const ImageView& src, const std::vector<std::int16_t>& xy, const std::vector<std::uint16_t>& f,
+                           int rows, int cols, ColorImage& dst) {
+        dst.rows = rows;
+        dst.cols = cols;
+        dst.data.assign((std::size_t)rows * cols * 3, 0);
+        detail::ops_check(tsm_remap_linear_fixed(src.data, src.rows, src.cols, src.step, 3, xy.data(),
+                                                 (std::size_t)cols * 4, f.data(), (std::size_t)cols * 2, rows, cols,
+                                                 dst.data.data(), (std::size_t)cols * 3),
+                          "rectify");
+    }
+#endif
 };
 
 }  // namespace stereo

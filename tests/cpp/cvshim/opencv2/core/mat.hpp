@@ -11,12 +11,22 @@
 #include <vector>
 
 #define CV_8U 0
+#define CV_8S 1
+#define CV_16U 2
+#define CV_16S 3
+#define CV_32S 4
 #define CV_32F 5
+#define CV_64F 6
 #define CV_CN_SHIFT 3
 #define CV_MAKETYPE(depth, cn) ((depth) + (((cn) - 1) << CV_CN_SHIFT))
 #define CV_8UC1 CV_MAKETYPE(CV_8U, 1)
 #define CV_8UC3 CV_MAKETYPE(CV_8U, 3)
+#define CV_16UC1 CV_MAKETYPE(CV_16U, 1)
+#define CV_16SC1 CV_MAKETYPE(CV_16S, 1)
+#define CV_16SC2 CV_MAKETYPE(CV_16S, 2)
 #define CV_32FC1 CV_MAKETYPE(CV_32F, 1)
+#define CV_32FC3 CV_MAKETYPE(CV_32F, 3)
+#define CV_64FC1 CV_MAKETYPE(CV_64F, 1)
 
 namespace cv {
 
@@ -81,7 +91,11 @@ public:
     }
     int type() const { return type_; }
     int channels() const { return 1 + (type_ >> CV_CN_SHIFT); }
-    std::size_t elemSize() const { return (std::size_t)channels() * ((type_ & 7) == CV_32F ? 4 : 1); }
+    std::size_t elemSize1() const {
+        static const std::size_t sz[8] = {1, 1, 2, 2, 4, 4, 8, 2};
+        return sz[type_ & 7];
+    }
+    std::size_t elemSize() const { return (std::size_t)channels() * elemSize1(); }
     bool empty() const { return data == nullptr || rows == 0 || cols == 0; }
     Size size() const { return Size(cols, rows); }
     bool isContinuous() const { return step.p[0] == (std::size_t)cols * elemSize(); }

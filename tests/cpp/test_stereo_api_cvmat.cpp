@@ -6,6 +6,8 @@
 // TSM_HAVE_OPENCV branch.  Run by tests/test_gpu_cpp_api.py on the GPU box, which compares
 // the disparity with the oracle bit for bit.
 #include <cstdio>
+#include <array>
+#include <cstdint>
 #include <cstring>
 #include <string>
 #include <vector>
@@ -140,6 +142,101 @@ int main(int argc, char** argv) {
     CHECK(out.ptr<float>(H - 1)[W - 1] == 7.f);
     matchers[0]->compute(L, R, out);
     CHECK(same_bits(out, Dc));
+
+    // ---- the calls either side of the matcher in the reference's cv::Mat signatures
+    // (reference stereo.h:194-296), each equal to the light form on the same data
+    const cv::Mat jet = stereo::JETColorMap();
+    const stereo::ColorMapTable jt = stereo::JETColorMapTable();
+    CHECK(jet.rows == 1 && jet.cols == 256 && jet.type() == CV_8UC3 &&
+          std::memcmp(jet.ptr(0), jt.data(), 768) == 0);
+    stereo::DisparityMap dl;  // the light copy of D
+    dl.rows = H;
+    dl.cols = W;
+    dl.data.assign(D.ptr<float>(0), D.ptr<float>(0) + (size_t)H * W);
+    auto same_bytes = [](const cv::Mat& m, const void* p, size_t rowb) {
+        for (int y = 0; y < m.rows; ++y)
+            if (std::memcmp(m.ptr(y), (const char*)p + (size_t)y * rowb, rowb) != 0) return false;
+        return true;
+    };
+    cv::Mat vis, vis2;
+    stereo::applyColorMap(D, vis, jet);
+    stereo::ColorImage cvis;
+    stereo::applyColorMap(dl, cvis, jt);
+    CHECK(vis.type() == CV_8UC3 && vis.rows == H && same_bytes(vis, cvis.data.data(), (size_t)W * 3));
+    stereo::applyColorMap(D, vis2, 2.f, 12.f, jet);
+    stereo::applyColorMap(dl, cvis, 2.f, 12.f, jt);
+    CHECK(same_bytes(vis2, cvis.data.data(), (size_t)W * 3));
+    cv::Mat depth;
+    stereo::reprojectToDepth(D, 700.f, 0.1f, depth);
+    stereo::DisparityMap ldepth;
+    stereo::reprojectToDepth(dl, 700.f, 0.1f, ldepth);
+    CHECK(depth.type() == CV_32FC1 && same_bytes(depth, ldepth.data.data(), (size_t)W * 4));
+    cv::Mat xyz, xyzq, xyzq32;
+    stereo::reprojectTo3D(D, 700.f, 0.1f, W / 2.f, H / 2.f, xyz);
+    stereo::PointImage lxyz;
+    stereo::reprojectTo3D(dl, 700.f, 0.1f, W / 2.f, H / 2.f, lxyz);
+    CHECK(xyz.type() == CV_32FC3 && same_bytes(xyz, lxyz.data.data(), (size_t)W * 12));
+    const std::array<double, 16> q = {1, 0, 0, -W / 2.0, 0, 1, 0, -H / 2.0, 0, 0, 0, 700, 0, 0, 10, 0};
+    cv::Mat Q(4, 4, CV_64FC1), Q32(4, 4, CV_32FC1);
+    for (int i = 0; i < 16; ++i) {
+        Q.ptr<double>(i / 4)[i % 4] = q[i];
+        Q32.ptr<float>(i / 4)[i % 4] = (float)q[i];
+    }
+    stereo::reprojectTo3D(D, Q, xyzq);
+    stereo::reprojectTo3D(D, Q32, xyzq32);
+    stereo::reprojectTo3D(dl, q, lxyz);
+    CHECK(same_bytes(xyzq, lxyz.data.data(), (size_t)W * 12) && same_bytes(xyzq32, lxyz.data.data(), (size_t)W * 12));
+    // point clouds: the cv::Mat writers' files are byte-identical to the light writers'
+    auto slurp = [](const char* path) {
+        std::string s;
+        if (FILE* f = std::fopen(path, "rb")) {
+            char buf[4096];
+            size_t n;
+            while ((n = std::fread(buf, 1, sizeof buf, f)) > 0) s.append(buf, n);
+            std::fclose(f);
+        }
+        return s;
+    };
+    stereo::reprojectTo3D(dl, 700.f, 0.1f, W / 2.f, H / 2.f, lxyz);
+    stereo::writePointCloudToPLY(L, xyz, "/tmp/tsm_cvmat_cloud.ply");
+    stereo::writePointCloudToPLY(stereo::ImageView{L.data, H, W, L.step[0]}, lxyz, "/tmp/tsm_light_cloud.ply");
+    stereo::writePointCloudToPCD(L, xyz, "/tmp/tsm_cvmat_cloud.pcd");
+    stereo::writePointCloudToPCD(stereo::ImageView{L.data, H, W, L.step[0]}, lxyz, "/tmp/tsm_light_cloud.pcd");
+    const std::string ply = slurp("/tmp/tsm_cvmat_cloud.ply"), pcd = slurp("/tmp/tsm_cvmat_cloud.pcd");
+    CHECK(ply.size() > 100 && ply == slurp("/tmp/tsm_light_cloud.ply"));
+    CHECK(pcd.size() > 100 && pcd == slurp("/tmp/tsm_light_cloud.pcd"));
+    // rectification with the reference's map types: identity CV_16SC2 + CV_16UC1 maps and
+    // identity CV_32FC1 map pairs return their inputs
+    cv::Mat m00(H, W, CV_16SC2), m01(H, W, CV_16UC1), fx(H, W, CV_32FC1), fy(H, W, CV_32FC1);
+    for (int y = 0; y < H; ++y)
+        for (int x = 0; x < W; ++x) {
+            m00.ptr<int16_t>(y)[2 * x] = (int16_t)x;
+            m00.ptr<int16_t>(y)[2 * x + 1] = (int16_t)y;
+            m01.ptr<uint16_t>(y)[x] = 0;
+            fx.ptr<float>(y)[x] = (float)x;
+            fy.ptr<float>(y)[x] = (float)y;
+        }
+    const cv::Mat empty_mat;
+    stereo::EpipolarRectifyMap rm(empty_mat, empty_mat, empty_mat, empty_mat, m00, m01, m00, m01);
+    stereo::EpipolarRectify rect(rm, cv::Size(W, H));
+    cv::Mat rl, rr, side;
+    rect.rectify(Lc, Rc, rl, rr);
+    CHECK(same_bits(rl, Lc) && same_bits(rr, Rc));
+    cv::Mat sbs(H, 2 * W, CV_8UC3);  // side by side: left | right
+    for (int y = 0; y < H; ++y) {
+        std::memcpy(sbs.ptr(y), Lc.ptr(y), (size_t)W * 3);
+        std::memcpy(sbs.ptr(y) + (size_t)W * 3, Rc.ptr(y), (size_t)W * 3);
+    }
+    rect.rectify(sbs, side);
+    CHECK(same_bits(side, sbs));
+    stereo::EpipolarRectify rectf(stereo::EpipolarRectifyMap(empty_mat, empty_mat, empty_mat, empty_mat, fx, fy, fx, fy),
+                                  cv::Size(W, H));
+    rectf.rectify(Lc, Rc, rl, rr);
+    CHECK(same_bits(rl, Lc) && same_bits(rr, Rc));
+    bool threw = false;
+    try { stereo::EpipolarRectify().loadEpipolarRectifyMap(stereo::EpipolarRectifyMap{}, cv::Size(W, H)); }
+    catch (const std::runtime_error& e) { threw = std::string(e.what()) == "stereo params is empty, please load it first"; }
+    CHECK(threw);
 
     std::printf("%s (%d failures)\n", fails ? "FAILED" : "OK", fails);
     return fails ? 1 : 0;
