@@ -643,6 +643,11 @@ int run_pipeline(tsm_adc* h, Workspace* w, int K, const PairIn& in, size_t step,
     if (keep_view1 && (rc = dump_vol(dump->cost_scan, 2)) != TSM_OK) return rc;
     if (dump && dump->wta && (rc = d2h(dump->wta, w->rb.disp0, 2 * N * 4)) != TSM_OK) return rc;
     // --- refinement --------------------------------------------------------------------
+#ifdef TSM_EXP_NO_REFINE  // timing probe (make exp): what the refinement chain costs a group
+    mark_stage();
+    if (h->profiling) w->pending.emplace_back(ev, K);
+    return TSM_OK;
+#endif
     launch_outlier(w->rb, P, st);
     if (dump && dump->outlier && (rc = d2h(dump->outlier, w->rb.dm, N * 4)) != TSM_OK) return rc;
     {

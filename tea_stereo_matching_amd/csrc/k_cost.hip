@@ -207,6 +207,16 @@ __device__ __forceinline__ uint32_t bcnt_acc(uint32_t x, uint32_t acc) {
     return r;
 }
 
+// HSI AD table index (computeHSIADCost :439-451 with the lambdas 1, 2.5, 2.5 the engine
+// requires, doubled: the table holds k / 2): 2 * circular hue distance + 5 * (|dS| + |dI|),
+// the factor 5 as a 24-bit multiply (the compiler otherwise picks the quarter-rate
+// v_mul_lo_u32)
+__device__ __forceinline__ int hsi_ad(uint32_t fc, uint32_t vc) {
+    const uint32_t hd = __builtin_amdgcn_sad_u8(fc & 0xffu, vc & 0xffu, 0u);
+    const uint32_t si = __builtin_amdgcn_sad_u8(fc & 0xffff00u, vc & 0xffff00u, 0u);
+    return (int)(2u * min(hd, 255u - hd) + __umul24(si, 5u));
+}
+
 // labels one walk unit covers: 64 E, the tail float4 aside
 __host__ __device__ constexpr int cw_slice(int E) { return 64 * E; }
 
@@ -359,17 +369,16 @@ __global__ __launch_bounds__(CW_THREADS) __attribute__((amdgpu_waves_per_eu(E ==
 #pragma unroll
                         for (int w = 0; w < 6; ++w) cen = bcnt_acc((Fr[w] & Vr[6 + w]) | (Fr[6 + w] & Vr[w]), cen);
                     } else {
-                        cen = __builtin_popcount(~(Fr[0] & Vr[0])) + __builtin_popcount(~(Fr[1] & Vr[1]) & vmask_hi);
+                        cen = bcnt_acc(~(Fr[1] & Vr[1]) & vmask_hi, bcnt_acc(~(Fr[0] & Vr[0]), 0u));
 #pragma unroll
-                        for (int w = 2; w < 6; ++w) cen += __builtin_popcount((Fr[w] & Vr[4 + w]) | (Fr[4 + w] & Vr[w]));
+                        for (int w = 2; w < 6; ++w) cen = bcnt_acc((Fr[w] & Vr[4 + w]) | (Fr[4 + w] & Vr[w]), cen);
                     }
                     const uint32_t vc = Vr[NW - 1], fc = Fr[NW - 1];
                     int ai;
                     if (!HSI) {
                         ai = (int)__builtin_amdgcn_sad_u8(fc, vc, 0u);
                     } else {
-                        const int hd = (int)__builtin_amdgcn_sad_u8(fc & 0xffu, vc & 0xffu, 0u);
-                        ai = 2 * min(hd, 255 - hd) + 5 * (int)__builtin_amdgcn_sad_u8(fc & 0xffff00u, vc & 0xffff00u, 0u);
+                        ai = hsi_ad(fc, vc);
                     }
                     const float c = sA[ai] - sB[cen];
                     c4[t] = (fixed_ok && k >= klo && k <= khi) ? c : 2.f;
@@ -419,16 +428,24 @@ __global__ __launch_bounds__(CW_THREADS) __attribute__((amdgpu_waves_per_eu(E ==
                     const int s = UP ? (e - R + E) % E : (e + R) % E;
                     cen[e] = bcnt_acc((F[k] & V[6 + k][s]) | (F[6 + k] & V[k][s]), cen[e]);
                 }
-        } else {
+        } else {  // hue: NAND of the positive-class planes (:489-492), then 4 gt/lt words
 #pragma unroll
             for (int e = 0; e < E; ++e) {
                 const int s = UP ? (e - R + E) % E : (e + R) % E;
-                cen[e] = padoff[e] + __builtin_popcount(~(F[0] & V[0][s])) +
-                         __builtin_popcount(~(F[1] & V[1][s]) & vmask_hi);
-#pragma unroll
-                for (int k = 2; k < 6; ++k)
-                    cen[e] += __builtin_popcount((F[k] & V[4 + k][s]) | (F[4 + k] & V[k][s]));
+                cen[e] = bcnt_acc(~(F[0] & V[0][s]), cen[e]);
             }
+#pragma unroll
+            for (int e = 0; e < E; ++e) {
+                const int s = UP ? (e - R + E) % E : (e + R) % E;
+                cen[e] = bcnt_acc(~(F[1] & V[1][s]) & vmask_hi, cen[e]);
+            }
+#pragma unroll
+            for (int k = 2; k < 6; ++k)
+#pragma unroll
+                for (int e = 0; e < E; ++e) {
+                    const int s = UP ? (e - R + E) % E : (e + R) % E;
+                    cen[e] = bcnt_acc((F[k] & V[4 + k][s]) | (F[4 + k] & V[k][s]), cen[e]);
+                }
         }
         float c[E];
 #pragma unroll
@@ -439,9 +456,7 @@ __global__ __launch_bounds__(CW_THREADS) __attribute__((amdgpu_waves_per_eu(E ==
             if (!HSI) {
                 ai = (int)__builtin_amdgcn_sad_u8(fc, vc, 0u);
             } else {
-                const int hd = (int)__builtin_amdgcn_sad_u8(fc & 0xffu, vc & 0xffu, 0u);
-                ai = 2 * min(hd, 255 - hd) +
-                     5 * (int)__builtin_amdgcn_sad_u8(fc & 0xffff00u, vc & 0xffff00u, 0u);
+                ai = hsi_ad(fc, vc);
             }
             // mask mode: black centre on either side -> census = +inf (:459-460)
             if (MASK && (fc == 0 || vc == 0)) cen[e] = 187;
@@ -467,7 +482,11 @@ __global__ __launch_bounds__(CW_THREADS) __attribute__((amdgpu_waves_per_eu(E ==
 #pragma unroll
             for (int e = 0; e < E; ++e) c[e] = kb + E * lane + e >= L ? kInf : c[e];
         }
+#ifdef TSM_EXP_COST_NOSTORE  // timing probe (make exp): the walk without its volume stores
+        if ((fast || t < count) && c[0] == -1.f) {
+#else
         if (fast || t < count) {
+#endif
             if constexpr (E == 3) {  // labels 3l .. 3l+2: one 12-B store per lane, 768 B a pixel
                 F3 o3;
                 o3.a = c[0];
