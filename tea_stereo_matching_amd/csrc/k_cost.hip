@@ -532,9 +532,16 @@ __global__ __launch_bounds__(CW_THREADS) __attribute__((amdgpu_waves_per_eu(E ==
             (step(IC<Ss>{}, fast, t + Ss), ...);
         }(std::make_integer_sequence<int, G>{});
         // the group's tail float4s (labels 64E .. 64E+3), lane s for pixel j0 + t + s, a
-        // few steps after those pixels' main stores: both still in L2
-        if (tail && lane < G && t + lane < count)
-            *reinterpret_cast<f32x4*>(vol + (((size_t)v * H + y) * W + j0 + t + lane) * Lp + 64 * E) = stT[t + lane];
+        // few steps after those pixels' main stores: both still in L2.  The lane id is
+        // recomputed here (2 VALU): held across the walk it was the register the allocator
+        // spilled, and the reload's wait (vmcnt, in order with the volume stores) then
+        // drained every group's stores before the walk went on.
+        if (tail) {
+            int ln;
+            asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0" : "=v"(ln));
+            if (ln < G && t + ln < count)
+                *reinterpret_cast<f32x4*>(vol + (((size_t)v * H + y) * W + j0 + t + ln) * Lp + 64 * E) = stT[t + ln];
+        }
     }
     };
     // slices whose lane labels are all real (config B: 192 of 193) keep no padding offsets
