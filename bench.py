@@ -398,7 +398,7 @@ def configs_leg(tsm, dev, b_lefts, b_rights, reps=2):
     res = {}
     for name, desc, H, W, D, model, omp, grey, seed0, n, K, key in CONFIGS:
         L = D + 1
-        if (H, W) == (375, 1242) and seed0 == 1000:
+        if (H, W) == (375, 1242) and seed0 == 1000 and len(b_lefts) >= n:  # the main batch's pairs
             lefts, rights = b_lefts[:n], b_rights[:n]
         else:
             lefts, rights = [], []

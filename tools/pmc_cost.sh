@@ -6,7 +6,7 @@ set -u
 cd /tmp && export TMPDIR=/tmp && cd "${GRAFT_REPO_ROOT}"
 mkdir -p gpurun_out
 RX=${1:-cost_tile}
-B="python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline --no-ops --batch 2 --concurrency 1"
+B="python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline --no-ops --no-configs --batch 2 --concurrency 1"
 timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE --kernel-include-regex "$RX" --output-format csv -d gpurun_out/pmc_cost_fetch -o run -- $B > gpurun_out/pmc_cost_fetch.log 2>&1
 rc=$?; echo "fetch rc=$rc"; [ $rc -ne 0 ] && { tail -5 gpurun_out/pmc_cost_fetch.log; exit $rc; }
 timeout -s KILL 120 rocprofv3 --pmc WRITE_SIZE --kernel-include-regex "$RX" --output-format csv -d gpurun_out/pmc_cost_write -o run -- $B > gpurun_out/pmc_cost_write.log 2>&1
