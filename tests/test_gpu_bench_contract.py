@@ -1,0 +1,40 @@
+"""bench.py's one-line JSON contract, run end to end on the GPU at a small batch.
+
+The driver runs `python bench.py` with no flags at round end; this runs the same script
+(one step of two pairs, groups of one) and checks the fields the driver and the judge
+read: metric / value / unit, the timing fields, `roofline` and the self-verification of
+pair 0 against the oracle's golden hash.  The CPU baseline, the f2-f4 leg and the configs
+block are skipped here (their own legs are exercised by the full bench run).
+"""
+import json
+import os
+import subprocess
+import sys
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+@pytest.mark.gpu
+def test_bench_json_line_small_batch():
+    cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--steps", "1", "--warmup", "1", "--batch", "2",
+           "--concurrency", "1", "--no-cpu-baseline", "--no-ops", "--no-configs"]
+    p = subprocess.run(cmd, cwd=ROOT, capture_output=True, text=True, timeout=240)
+    assert p.returncode == 0, p.stderr[-2000:]
+    lines = [l for l in p.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1, p.stdout[-2000:]
+    d = json.loads(lines[0])
+    assert d["unit"] == "pairs/s" and d["metric"].startswith("stereo pairs/s")
+    assert d["value"] > 0 and d["n_gpus"] == 1 and d["steps"] == 1 and d["warmup"] == 1
+    assert d["higher_is_better"] is True and d["scaling"] == "weak" and d["vs_baseline"] is None
+    assert d["dtype"] == "f32" and d["config"]["workload"].startswith("config B")
+    assert d["config"]["pairs_per_gpu_per_step"] == 2
+    # value is the whole job's pairs over the timed region
+    assert abs(d["value"] - 2 / (d["ms_per_step"] / 1e3)) / d["value"] < 0.02
+    r = d["roofline"]
+    assert r["bound"] == "hbm" and r["unit"] == "GB/s" and r["peak"] == 8000.0
+    assert 0 < r["frac"] < 1 and abs(r["frac"] - r["achieved"] / r["peak"]) < 1e-3
+    assert r["algorithmic_bytes_per_launch"] == 4 * 193 * 1242 * 375 * 2 + 2 * 3 * 1242 * 375
+    assert d["verified"] is True, d.get("verification")
+    assert d["library"].endswith("libtsm_adcensus.so")
