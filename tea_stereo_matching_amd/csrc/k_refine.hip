@@ -95,6 +95,8 @@ __device__ __forceinline__ void block_scan2(int& a, int& b, int* sa, int* sb) {
 
 
 constexpr int VD_THREADS = 512;  // the vote decision: threads a high-vote outlier
+constexpr int RW_B = 8;          // region walks: row-segment pixels loaded a round trip (minD >= 0,
+                                 // so -1 marks a slot past the segment)
 
 
 // ---------------------------------------------------------------------------
@@ -204,12 +206,18 @@ __global__ __launch_bounds__(256) void k_vote_count_rank(const int32_t* __restri
                 region_arms(arms[(size_t)yy0 * W + xx0], hf, a1, b1, a2, b2);
                 const ptrdiff_t st = hf ? 1 : W;
                 const int32_t* rp = disp + (size_t)yy0 * W + xx0;
-                for (int i = -a2; i <= b2; ++i) {
-                    const int dv = rp[(ptrdiff_t)i * st];
-                    if (dv >= minD) {
-                        if (emit) smp[pos + cnt] = (uint16_t)(dv - minD);
-                        cnt++;
-                    }
+                // the row segment RW_B pixels a round trip (loads issued back to back, then
+                // used in order: the samples keep the reference's order)
+                for (int i = -a2; i <= b2; i += RW_B) {
+                    int dv[RW_B];
+#pragma unroll
+                    for (int k = 0; k < RW_B; ++k) dv[k] = i + k <= b2 ? rp[(ptrdiff_t)(i + k) * st] : -1;
+#pragma unroll
+                    for (int k = 0; k < RW_B; ++k)
+                        if (dv[k] >= minD) {
+                            if (emit) smp[pos + cnt] = (uint16_t)(dv[k] - minD);
+                            cnt++;
+                        }
                 }
             }
             return cnt;
@@ -339,9 +347,13 @@ __global__ __launch_bounds__(VD_THREADS) void k_vote_decide_rank(
                     region_arms(arms[(size_t)yy0 * W + xx0], hf, a1, b1, a2, b2);
                     const ptrdiff_t st = hf ? 1 : W;
                     const int32_t* rp = disp + (size_t)yy0 * W + xx0;
-                    for (int i = -a2; i <= b2; ++i) {
-                        const int dv = rp[(ptrdiff_t)i * st];
-                        if (dv >= minD) atomicAdd(&h[dv - minD], 1);
+                    for (int i = -a2; i <= b2; i += RW_B) {  // RW_B loads a round trip
+                        int dv[RW_B];
+#pragma unroll
+                        for (int k = 0; k < RW_B; ++k) dv[k] = i + k <= b2 ? rp[(ptrdiff_t)(i + k) * st] : -1;
+#pragma unroll
+                        for (int k = 0; k < RW_B; ++k)
+                            if (dv[k] >= minD) atomicAdd(&h[dv[k] - minD], 1);
                     }
                 }
             }
