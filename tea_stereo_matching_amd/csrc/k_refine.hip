@@ -95,6 +95,7 @@ __device__ __forceinline__ void block_scan2(int& a, int& b, int* sa, int* sb) {
 
 
 constexpr int VD_THREADS = 512;  // the vote decision: threads a high-vote outlier
+constexpr int RI_B = 4;          // interpolation rays: steps loaded a round trip
 constexpr int RW_B = 8;          // region walks: row-segment pixels loaded a round trip (minD >= 0,
                                  // so -1 marks a slot past the segment)
 
@@ -444,16 +445,34 @@ __global__ __launch_bounds__(256) void k_interp_rays(const int32_t* __restrict__
         const uint32_t c0 = img0[idx];
         const int rh = c_ray_h[dir], rw = c_ray_w[dir];
         const int sh0 = rh / 2, sh1 = rh - rh / 2, sw0 = rw / 2, sw1 = rw - rw / 2;
+        // RI_B steps a round trip: their positions, then their loads back to back, then the
+        // first in-image valid one in step order (a ray moves monotonically, so it never
+        // re-enters the image once it has left it)
         int hD = y, wD = x;
-        for (int s = 0; s < P.max_search_depth; ++s) {
-            hD += (s & 1) ? sh1 : sh0;
-            wD += (s & 1) ? sw1 : sw0;
-            if (hD < 0 || hD >= H || wD < 0 || wD >= W) break;
-            const int dv = disp[(size_t)hD * W + wD];
-            if (dv >= minD) {
-                nd = dv;
-                ndiff = color_diff(P, c0, img0[(size_t)hD * W + wD]);
-                break;
+        bool done = false;
+        for (int s0 = 0; s0 < P.max_search_depth && !done; s0 += RI_B) {
+            size_t at[RI_B];
+            bool ok[RI_B];
+            int dv[RI_B];
+#pragma unroll
+            for (int k = 0; k < RI_B; ++k) {
+                const int s = s0 + k;
+                hD += (s & 1) ? sh1 : sh0;
+                wD += (s & 1) ? sw1 : sw0;
+                ok[k] = s < P.max_search_depth && hD >= 0 && hD < H && wD >= 0 && wD < W;
+                at[k] = ok[k] ? (size_t)hD * W + wD : idx;
+            }
+#pragma unroll
+            for (int k = 0; k < RI_B; ++k) dv[k] = ok[k] ? disp[at[k]] : 0;
+#pragma unroll
+            for (int k = 0; k < RI_B; ++k) {
+                if (done) break;
+                if (!ok[k]) { done = true; break; }
+                if (dv[k] >= minD) {
+                    nd = dv[k];
+                    ndiff = color_diff(P, c0, img0[at[k]]);
+                    done = true;
+                }
             }
         }
     }
