@@ -22,17 +22,30 @@ namespace tsm {
 
 // computeLimit, ADCensus.cpp:604-659 (returns the arm length; one shorter when the walk
 // ends at the image border, :650-658).  p: the pixel; fetch(k): the pixel k steps along the
-// arm's direction; avail: how many such steps stay inside the image.
+// arm's direction; avail: how many such steps stay inside the image.  The walk loads
+// ARM_B pixels a round trip (those inside the image), then takes its steps over them in
+// order with the reference's conditions; the loads past where the walk stops go unused.
+constexpr int ARM_B = 4;
 template <class F>
 __device__ __forceinline__ int compute_limit(const DevParams& P, uint32_t p, int avail, F fetch) {
     int d = 1;
     uint32_t p2 = p;
-    bool inside = 1 <= avail;
-    if (inside) {
-        bool colorCond = true, wLimitCond = true, fColorCond = true;
-        while (colorCond && wLimitCond && fColorCond && inside) {
-            const uint32_t p1 = fetch(d);
-            if (P.mask && p1 == 0) { d++; break; } // :625-629
+    bool go = 1 <= avail;
+    const bool any = go;
+    while (go) {
+        uint32_t q[ARM_B];
+#pragma unroll
+        for (int k = 0; k < ARM_B; ++k) q[k] = d + k <= avail ? fetch(d + k) : 0u;
+#pragma unroll
+        for (int k = 0; k < ARM_B; ++k) {
+            if (!go) break;
+            const uint32_t p1 = q[k];
+            if (P.mask && p1 == 0) {  // :625-629
+                d++;
+                go = false;
+                break;
+            }
+            bool colorCond, fColorCond;
             if (P.color_model == 0) {
                 colorCond = color_diff(P, p, p1) < P.color_thresh1 &&
                             color_diff(P, p1, p2) < P.color_thresh1;
@@ -46,13 +59,14 @@ __device__ __forceinline__ int compute_limit(const DevParams& P, uint32_t p, int
                 fColorCond = (d <= P.max_length2) ||
                              (d > P.max_length2 && iabs_(ch(p, 2) - ch(p1, 2)) < P.int_thresh2);
             }
-            wLimitCond = d < P.max_length1;
+            const bool wLimitCond = d < P.max_length1;
             p2 = p1;
-            inside = d + 1 <= avail;
+            const bool inside = d + 1 <= avail;
             d++;
+            go = colorCond && wLimitCond && fColorCond && inside;
         }
-        d--;
     }
+    if (any) d--;
     return d - 1;
 }
 
