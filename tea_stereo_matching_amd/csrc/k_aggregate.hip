@@ -119,14 +119,23 @@ __global__ void k_window_sizes(const uint32_t* __restrict__ arms, int32_t* __res
     pair_shift(blockIdx.z >> 1, P.pstride, arms, ws);
     const uint32_t* A = arms + (size_t)v * H * W;
     const uint32_t a = A[(size_t)y * W + x];
+    // integer sums (any order): ARM_B arms loaded a round trip
     int hf = 0, vf = 0;
-    for (int k = -arm_up(a); k <= arm_down(a); ++k) {
-        const uint32_t b = A[(size_t)(y + k) * W + x];
-        hf += arm_left(b) + arm_right(b) + 1;
+    for (int k0 = -arm_up(a); k0 <= arm_down(a); k0 += ARM_B) {
+        uint32_t b[ARM_B];
+#pragma unroll
+        for (int j = 0; j < ARM_B; ++j) b[j] = k0 + j <= arm_down(a) ? A[(size_t)(y + k0 + j) * W + x] : 0xffffffffu;
+#pragma unroll
+        for (int j = 0; j < ARM_B; ++j)
+            if (k0 + j <= arm_down(a)) hf += arm_left(b[j]) + arm_right(b[j]) + 1;
     }
-    for (int k = -arm_left(a); k <= arm_right(a); ++k) {
-        const uint32_t b = A[(size_t)y * W + (x + k)];
-        vf += arm_up(b) + arm_down(b) + 1;
+    for (int k0 = -arm_left(a); k0 <= arm_right(a); k0 += ARM_B) {
+        uint32_t b[ARM_B];
+#pragma unroll
+        for (int j = 0; j < ARM_B; ++j) b[j] = k0 + j <= arm_right(a) ? A[(size_t)y * W + (x + k0 + j)] : 0xffffffffu;
+#pragma unroll
+        for (int j = 0; j < ARM_B; ++j)
+            if (k0 + j <= arm_right(a)) vf += arm_up(b[j]) + arm_down(b[j]) + 1;
     }
     ws[((size_t)(v * 2 + 0) * H + y) * W + x] = hf;
     ws[((size_t)(v * 2 + 1) * H + y) * W + x] = vf;
