@@ -74,6 +74,21 @@ __device__ __forceinline__ void region_arms(uint32_t a, bool hf, int& oA, int& o
 // k_oscan_scatter with the preceding blocks' counts).
 constexpr int SC_THREADS = 256, SC_ITEMS = 16, SC_BLOCK = SC_THREADS * SC_ITEMS;
 
+// the SC_ITEMS disparities of a thread (16-B loads when the run is whole; the buffers are
+// 256-B aligned); past n: INT_MAX, never an outlier
+__device__ __forceinline__ void load_items(const int32_t* __restrict__ disp, int base, int n, int (&dv)[SC_ITEMS]) {
+    if (base + SC_ITEMS <= n) {
+#pragma unroll
+        for (int k = 0; k < SC_ITEMS; k += 4) {
+            const int4 v = *reinterpret_cast<const int4*>(disp + base + k);
+            dv[k] = v.x; dv[k + 1] = v.y; dv[k + 2] = v.z; dv[k + 3] = v.w;
+        }
+    } else {
+#pragma unroll
+        for (int k = 0; k < SC_ITEMS; ++k) dv[k] = base + k < n ? disp[base + k] : 0x7fffffff;
+    }
+}
+
 __device__ __forceinline__ void block_scan2(int& a, int& b, int* sa, int* sb) {
     // inclusive scan over the block of (a, b), returns exclusive prefix; totals in sa/sb[SC_THREADS]
     const int t = threadIdx.x;
@@ -114,11 +129,11 @@ __global__ void k_oscan_count(const int32_t* __restrict__ disp, int n, int minD,
     pair_shift(blockIdx.z, ps, disp, bsum);
     __shared__ int sa[SC_THREADS], sb[SC_THREADS];
     const int base = blockIdx.x * SC_BLOCK + threadIdx.x * SC_ITEMS;
+    int dv[SC_ITEMS];
+    load_items(disp, base, n, dv);
     int a = 0, b = 0;
-    for (int k = 0; k < SC_ITEMS; ++k) {
-        const int p = base + k;
-        if (p < n && disp[p] < minD) a++;
-    }
+#pragma unroll
+    for (int k = 0; k < SC_ITEMS; ++k) a += dv[k] < minD ? 1 : 0;
     block_scan2(a, b, sa, sb);
     if (threadIdx.x == SC_THREADS - 1) {
         bsum[2 * blockIdx.x] = sa[SC_THREADS - 1];
@@ -153,11 +168,11 @@ __global__ void k_oscan_scatter(const int32_t* __restrict__ disp, int n, int min
     if (threadIdx.x < VB_L1) vbits[(size_t)gridDim.x * VB_L0 + blockIdx.x * VB_L1 + threadIdx.x] = 0u;
     __shared__ int sa[SC_THREADS], sb[SC_THREADS];
     const int base = blockIdx.x * SC_BLOCK + threadIdx.x * SC_ITEMS;
+    int dv[SC_ITEMS];
+    load_items(disp, base, n, dv);
     int a = 0, b = 0;
-    for (int k = 0; k < SC_ITEMS; ++k) {
-        const int p = base + k;
-        if (p < n && disp[p] < minD) a++;
-    }
+#pragma unroll
+    for (int k = 0; k < SC_ITEMS; ++k) a += dv[k] < minD ? 1 : 0;
     block_scan2(a, b, sa, sb);  // its barriers also publish s_base
     const int first = s_base;
     a += first;
@@ -165,13 +180,16 @@ __global__ void k_oscan_scatter(const int32_t* __restrict__ disp, int n, int min
         counts[0] = first + sa[SC_THREADS - 1];
         counts[1] = 0;
     }
-    for (int k = 0; k < SC_ITEMS; ++k) {
-        const int p = base + k;
-        if (p >= n) break;
-        const int d = disp[p];
-        dtmp[p] = d;
-        if (d < minD) out_list[a++] = p;
+    if (base + SC_ITEMS <= n) {
+#pragma unroll
+        for (int k = 0; k < SC_ITEMS; k += 4)
+            *reinterpret_cast<int4*>(dtmp + base + k) = make_int4(dv[k], dv[k + 1], dv[k + 2], dv[k + 3]);
+    } else {
+        for (int k = 0; k < SC_ITEMS && base + k < n; ++k) dtmp[base + k] = dv[k];
     }
+#pragma unroll
+    for (int k = 0; k < SC_ITEMS; ++k)
+        if (dv[k] < minD) out_list[a++] = base + k;
 }
 
 // Vote count of every ranked outlier, 16 lanes an outlier (4 a wave), grid-stride over
