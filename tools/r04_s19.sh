@@ -4,7 +4,7 @@
 set -u
 cd /tmp && export TMPDIR=/tmp && cd "${GRAFT_REPO_ROOT}"
 mkdir -p gpurun_out
-T=r04_v4
+T=${1:-r04_v4}
 bash tools/r04_check.sh $T || exit $?
 timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/${T}_prof -o run -- python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline > gpurun_out/${T}_prof.log 2>&1
 rc=$?; echo "prof rc=$rc"; [ $rc -ne 0 ] && { tail -20 gpurun_out/${T}_prof.log; exit $rc; }
