@@ -39,12 +39,19 @@ $(LIB): $(OBJS)
 	@mkdir -p $(LIBDIR)
 	$(HIPCC) --offload-arch=$(ARCH) -shared -o $@ $(OBJS)
 
-# experimental variants for on-GPU A/B timing: make exp X=name DEFS="-DTSM_EXP_..."
+# experimental variants for on-GPU A/B timing, built from a copy of the sources with a
+# patch applied (the product sources carry no probes):
+#   make exp X=name PATCH=tools/probes/name.patch [DEFS=...]
+EXP = build/exp/$(X)
 exp:
-	@mkdir -p build/exp/$(X)/obj
-	for f in $(HIP_SRCS); do $(HIPCC) $(HIPFLAGS) $(DEFS) -c $(SRC)/$$f.hip -o build/exp/$(X)/obj/$$f.o || exit 1; done
-	for f in $(CPP_SRCS); do $(HIPCC) $(HIPFLAGS) $(DEFS) -c $(SRC)/$$f.cpp -o build/exp/$(X)/obj/$$f.o || exit 1; done
-	$(HIPCC) --offload-arch=$(ARCH) -shared -o build/exp/$(X)/libtsm_adcensus.so build/exp/$(X)/obj/*.o
+	rm -rf $(EXP)/tea_stereo_matching_amd $(EXP)/include $(EXP)/obj
+	mkdir -p $(EXP)/tea_stereo_matching_amd $(EXP)/obj
+	cp -r include $(EXP)/include
+	cp -r $(SRC) $(EXP)/tea_stereo_matching_amd/csrc
+	if [ -n "$(PATCH)" ]; then patch -p1 -d $(EXP) < $(PATCH) || exit 1; fi
+	for f in $(HIP_SRCS); do $(HIPCC) $(HIPFLAGS) $(DEFS) -c $(EXP)/$(SRC)/$$f.hip -o $(EXP)/obj/$$f.o || exit 1; done
+	for f in $(CPP_SRCS); do $(HIPCC) $(HIPFLAGS) $(DEFS) -c $(EXP)/$(SRC)/$$f.cpp -o $(EXP)/obj/$$f.o || exit 1; done
+	$(HIPCC) --offload-arch=$(ARCH) -shared -o $(EXP)/libtsm_adcensus.so $(EXP)/obj/*.o
 
 oracle:
 	$(MAKE) -C oracle

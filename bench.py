@@ -367,24 +367,49 @@ def main():
         dist.destroy_process_group()
 
 
-# The configs block: BASELINE.json's other single-GPU configs and the modes beside the
-# headline (untimed for `value`).  (name, workload, H, W, D, colour model, omp threads,
-# grey, first seed, pairs, pairs per group, golden-hash key of the first pair)
+# The configs block: BASELINE.json's other single-GPU configs, the reference's real pairs and
+# the modes beside the headline (untimed for `value`).  Per entry: name, workload, H, W, D,
+# colour model, omp threads, pairs, pairs per group, golden-hash key of pair 0, and the pair
+# source: ("syn", first seed, grey) -> synthetic seeds, ("noisy", first seed) -> config B
+# with +-3 noise on the right view, ("png", left, right) -> one real pair replicated.
 CONFIGS = [
-    ("C", "config C: 1500x1000 BGR, setMinMaxDisparity(0,256), RGB", 1000, 1500, 256, 0, 0, False, 2000, 16, 8, "C"),
-    ("E", "config E: 2048x1536 grey -> BGR, setMinMaxDisparity(0,320), RGB", 1536, 2048, 320, 0, 0, True, 3000, 8, 4, "E"),
-    ("B_HSI", "config B in the reference's default HSI model", 375, 1242, 192, 1, 0, False, 1000, 128, 64, "B_HSI_1000"),
+    ("C", "config C: 1500x1000 BGR, setMinMaxDisparity(0,256), RGB", 1000, 1500, 256, 0, 0, 16, 8, "C",
+     ("syn", 2000, False)),
+    ("E", "config E: 2048x1536 grey -> BGR, setMinMaxDisparity(0,320), RGB", 1536, 2048, 320, 0, 0, 8, 4, "E",
+     ("syn", 3000, True)),
+    ("B_HSI", "config B in the reference's default HSI model", 375, 1242, 192, 1, 0, 128, 64, "B_HSI_1000",
+     ("syn", 1000, False)),
     ("B_OMP20", "config B, RGB, setOmpEmulation(20): equals the reference's shipped outputs", 375, 1242, 192, 0, 20,
-     False, 1000, 128, 64, "B_OMP20_1000"),
+     128, 64, "B_OMP20_1000", ("syn", 1000, False)),
+    ("B_noisy", "config B with independent +-3 noise on the right view (no exact-zero costs: every scanline "
+     "vector is updated and stored, as on real pairs)", 375, 1242, 192, 0, 0, 128, 64, "B_NOISY_1000",
+     ("noisy", 1000)),
+    ("A_real", "configs[0]: the reference's demo-imgs/0600 pair (1280x720), setMinMaxDisparity(0,192), RGB, "
+     "serial scanline; the pair replicated", 720, 1280, 192, 0, 0, 64, 32, "A_0600",
+     ("png", "0600-Left.png", "0600-Right.png")),
+    ("A_real_OMP20", "the same with setOmpEmulation(20): the reference's shipped 0600_adcensus.png output",
+     720, 1280, 192, 0, 20, 64, 32, "A_0600_OMP20", ("png", "0600-Left.png", "0600-Right.png")),
+    ("MOTO_real", "config C's real pair: Middlebury Motorcycle (reference demo-imgs, 1482x994), "
+     "setMinMaxDisparity(0,256), RGB; the pair replicated", 994, 1482, 256, 0, 0, 16, 8, "MOTO",
+     ("png", "Motorcycle_Left.png", "Motorcycle_Right.png")),
 ]
+
+
+def _load_bgr(name):
+    import numpy as np
+    from PIL import Image
+
+    path = os.path.join(ROOT, "tests", "golden", "demo", name)
+    return np.ascontiguousarray(np.array(Image.open(path).convert("RGB"))[:, :, ::-1])
 
 
 def configs_leg(tsm, dev, b_lefts, b_rights, reps=2):
     """Per config: pairs/s and ms/frame of the device batch entry (inputs in HBM, groups of
     `K` pairs over the two group streams, `reps` batches after one warm-up, wall clock
-    around synchronised batches), one frame's device-resident latency, the cost walk's
-    launch time alone (HIP events, groups of one) against B_build, and pair 0's SHA-256
-    against the oracle's (tests/golden/config_hashes.json)."""
+    around synchronised batches), one frame's device-resident and host-image latency, the
+    per-stage times and the cost walk's launch time with one pipeline alone (HIP events,
+    groups of one) against B_build, the scanline stage against its algorithmic bytes, and
+    pair 0's SHA-256 against the oracle's (tests/golden/config_hashes.json)."""
     import hashlib
 
     import numpy as np
@@ -396,16 +421,29 @@ def configs_leg(tsm, dev, b_lefts, b_rights, reps=2):
     except OSError:
         gold = {}
     res = {}
-    for name, desc, H, W, D, model, omp, grey, seed0, n, K, key in CONFIGS:
+    for name, desc, H, W, D, model, omp, n, K, key, src in CONFIGS:
         L = D + 1
-        if (H, W) == (375, 1242) and seed0 == 1000 and len(b_lefts) >= n:  # the main batch's pairs
-            lefts, rights = b_lefts[:n], b_rights[:n]
+        lh = rh = None
+        if src[0] == "syn" and (H, W) == (375, 1242) and src[1] == 1000 and len(b_lefts) >= n:
+            lefts, rights = b_lefts[:n], b_rights[:n]  # the main batch's pairs
+        elif src[0] == "png":
+            lh, rh = _load_bgr(src[1]), _load_bgr(src[2])
+            assert lh.shape == (H, W, 3) and rh.shape == (H, W, 3), (name, lh.shape)
+            l0, r0 = torch.from_numpy(lh).to(dev), torch.from_numpy(rh).to(dev)
+            lefts, rights = [l0.clone() for _ in range(n)], [r0.clone() for _ in range(n)]
+            del l0, r0
         else:
-            lefts, rights = [], []
-            for l, r, _ in tsm.synthetic.make_scene_batch(range(seed0, seed0 + n), H, W, L,
-                                                          threads=min(16, os.cpu_count() or 1), grayscale=grey):
-                lefts.append(torch.from_numpy(l).to(dev))
-                rights.append(torch.from_numpy(r).to(dev))
+            if src[0] == "noisy":
+                from concurrent.futures import ThreadPoolExecutor
+
+                with ThreadPoolExecutor(min(16, os.cpu_count() or 1)) as ex:
+                    pairs = list(ex.map(lambda s: tsm.synthetic.config_b_noisy(s), range(src[1], src[1] + n)))
+            else:
+                pairs = tsm.synthetic.make_scene_batch(range(src[1], src[1] + n), H, W, L,
+                                                       threads=min(16, os.cpu_count() or 1), grayscale=src[2])
+            lefts = [torch.from_numpy(l).to(dev) for l, _, _ in pairs]
+            rights = [torch.from_numpy(r).to(dev) for _, r, _ in pairs]
+            del pairs
         outs = torch.empty((n, H, W), dtype=torch.float32, device=dev)
         lp = [t.data_ptr() for t in lefts]
         rp = [t.data_ptr() for t in rights]
@@ -434,7 +472,16 @@ def configs_leg(tsm, dev, b_lefts, b_rights, reps=2):
             m.compute_device_ptr(lp[i % n], rp[i % n], H, W, W * 3, op[i % n], W * 4)
             m.synchronize()
         single = (time.perf_counter() - t1) / 5 * 1e3
-        # the cost walk alone: groups of one, HIP events around each launch
+        # the same frame through ADCensus::compute on host images (PCIe both ways)
+        if lh is None:
+            lh, rh = lefts[0].cpu().numpy(), rights[0].cpu().numpy()
+        single_host_out = m.compute(lh, rh)
+        t1 = time.perf_counter()
+        for _ in range(5):
+            single_host_out = m.compute(lh, rh)
+        single_host = (time.perf_counter() - t1) / 5 * 1e3
+        same_host = bool(np.array_equal(single_host_out, got0))
+        # one pipeline alone: per-stage times, the cost walk's launches (groups of one)
         m.setProfiling(True)
         m.resetStageTimes()
         k = min(n, 8)
@@ -447,21 +494,32 @@ def configs_leg(tsm, dev, b_lefts, b_rights, reps=2):
         t_cost = cost_ms / max(1, cost_n) / 1e3
         b_build = 4 * L * H * W * 2 + 2 * 3 * H * W
         ach = b_build / t_cost / 1e9 if t_cost > 0 else None
+        stage_ms = {kk: round(v[0] / max(1, v[1]), 4) for kk, v in st.items()}
+        vbytes = 2 * H * W * ((L + 3) // 4 * 4) * 4  # the two-view volume at the padded stride
+        scan = {}
+        if stage_ms.get("scanline", 0) > 0:
+            gbs = 7.5 * vbytes / (stage_ms["scanline"] * 1e-3) / 1e9
+            scan = {"transfers": 7.5, "ms_per_pair": stage_ms["scanline"], "achieved": round(gbs, 1),
+                    "frac": round(gbs / HBM_PEAK_GBS, 4)}
         res[name] = {
             "workload": desc, "pairs": n, "concurrency": K,
             "pairs_per_s": round(n * reps / dt, 3), "ms_per_frame": round(dt / (n * reps) * 1e3, 3),
             "single_frame_device_ms": round(single, 3),
+            "single_frame_host_ms": round(single_host, 3),
             "cost_walk": {"avg_launch_ms": round(t_cost * 1e3, 4), "algorithmic_bytes": b_build,
                           "achieved_GBps": round(ach, 1) if ach else None,
                           "frac": round(ach / HBM_PEAK_GBS, 4) if ach else None, "launches": cost_n},
-            "stage_ms_per_pair": {kk: round(v[0] / max(1, v[1]), 4) for kk, v in st.items()},
-            "verified": bool(verified),
-            "verification": f"pair 0 (seed {seed0}) SHA-256 == oracle's ({key})" if g else f"no golden hash {key}",
+            "stage_ms_per_pair": stage_ms,
+            "scanline_roofline": scan,
+            "verified": bool(verified and same_host),
+            "verification": (f"pair 0 SHA-256 == oracle's ({key}); host-image compute() == pair 0" if g
+                             else f"no golden hash {key}"),
         }
         del outs, lefts, rights
         torch.cuda.empty_cache()
     res["timing"] = (f"device batch entry, {reps} batches after one warm-up (wall clock, synchronised); "
-                     "single frame = mean of 5 device-resident compute() calls; cost walk = HIP events, groups of one")
+                     "single frame = mean of 5 compute() calls on device-resident / host images; "
+                     "stages and cost walk = HIP events, one pipeline, groups of one")
     return res
 
 

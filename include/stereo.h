@@ -25,12 +25,26 @@
 #include "tsm_adcensus.h"
 #include "tsm_stereo_ops.h"
 
-#if __has_include(<opencv2/core/mat.hpp>)
+// Which form is built is the includer's choice: -DTSM_WITH_OPENCV forces the cv::Mat form,
+// -DTSM_NO_OPENCV the light form; with neither, the cv::Mat form when the OpenCV header is
+// found.  Each form lives in its own inline namespace (stereo::cvmat_v1 / stereo::light_v1):
+// callers still write stereo::ADCensus, but a program whose translation units were compiled
+// in different forms fails to link (different mangled names) instead of mixing two vtable
+// layouts of one class at run time.
+#if defined(TSM_WITH_OPENCV) && defined(TSM_NO_OPENCV)
+#error "define at most one of TSM_WITH_OPENCV and TSM_NO_OPENCV"
+#endif
+#if defined(TSM_WITH_OPENCV) || (!defined(TSM_NO_OPENCV) && __has_include(<opencv2/core/mat.hpp>))
 #include <opencv2/core/mat.hpp>
 #define TSM_HAVE_OPENCV 1
 #endif
 
 namespace stereo {
+#ifdef TSM_HAVE_OPENCV
+inline namespace cvmat_v1 {
+#else
+inline namespace light_v1 {
+#endif
 
 /** stereo_utils.h:191-195 */
 enum class ColorModel { RGB = 0, HSI = 1 };
@@ -105,9 +119,13 @@ public:
      *  allocated CV_32FC1 disparity out (`disparity = m_floatDisparityMap.clone()`, :391:
      *  a Mat that shared the old buffer keeps its data). */
     void compute(const cv::Mat& leftImage, const cv::Mat& rightImage, cv::Mat& disparity) override {
-        if (leftImage.empty() || rightImage.empty() || leftImage.size() != rightImage.size() ||
-            leftImage.type() != CV_8UC3 || rightImage.type() != CV_8UC3)
-            throw(std::string("[ADCensus] Image error."));
+        if (leftImage.empty() || rightImage.empty() || leftImage.size() != rightImage.size())
+            throw(std::string("[ADCensus] Image error."));  // the reference's check (:332-333)
+        // a deliberate tightening: the reference reads any type as 3-byte BGR pixels; here a
+        // non-CV_8UC3 input is refused as an internal-error type, so callers catching the
+        // reference's std::string cases see them unchanged
+        if (leftImage.type() != CV_8UC3 || rightImage.type() != CV_8UC3)
+            throw std::runtime_error("[ADCensus] images must be CV_8UC3 (BGR u8)");
         cv::Mat out(leftImage.rows, leftImage.cols, CV_32FC1);
         run(view(leftImage), view(rightImage), out.ptr<float>(0), (std::size_t)out.step[0]);
         disparity = out;
@@ -120,8 +138,9 @@ public:
         for (std::size_t i = 0; i < leftImages.size(); ++i) {
             const cv::Mat& l = leftImages[i];
             const cv::Mat& r = rightImages[i];
-            if (l.empty() || r.empty() || l.size() != r.size() || l.type() != CV_8UC3 || r.type() != CV_8UC3)
-                throw(std::string("[ADCensus] Image error."));
+            if (l.empty() || r.empty() || l.size() != r.size()) throw(std::string("[ADCensus] Image error."));
+            if (l.type() != CV_8UC3 || r.type() != CV_8UC3)
+                throw std::runtime_error("[ADCensus] images must be CV_8UC3 (BGR u8)");
             ls.push_back(view(l));
             rs.push_back(view(r));
         }
@@ -604,4 +623,5 @@ private:
 #endif
 };
 
+}  // inline namespace cvmat_v1 / light_v1
 }  // namespace stereo

@@ -34,15 +34,38 @@
 using namespace tsm;
 
 namespace tsm {
-void trace_point(const char* what, hipStream_t st) {
+static bool trace_enabled() {
     static const bool trace = [] {  // read once (thread-safe static initialisation)
         const char* e = std::getenv("TSM_TRACE");
         return e && e[0] == '1';
     }();
-    if (!trace) return;
+    return trace;
+}
+
+uint32_t* trace_flag() {
+    if (!trace_enabled()) return nullptr;
+    static std::mutex mu;
+    static std::map<int, uint32_t*> per_dev;
+    int dev = 0;
+    (void)hipGetDevice(&dev);
+    std::lock_guard<std::mutex> g(mu);
+    uint32_t*& f = per_dev[dev];
+    if (!f && hipMalloc((void**)&f, 64) == hipSuccess) (void)hipMemset(f, 0, 64);
+    return f;
+}
+
+void trace_point(const char* what, hipStream_t st) {
+    if (!trace_enabled()) return;
     hipError_t le = hipGetLastError();
     hipError_t se = hipStreamSynchronize(st);
     std::fprintf(stderr, "[tsm] %-40s launch=%s sync=%s\n", what, hipGetErrorString(le), hipGetErrorString(se));
+    if (uint32_t* f = trace_flag()) {
+        uint32_t v[2] = {0, 0};
+        if (hipMemcpy(v, f, 8, hipMemcpyDeviceToHost) == hipSuccess && v[0] != 0) {
+            std::fprintf(stderr, "[tsm] %-40s PROTOCOL CHECK FAILED: kind=%u detail=0x%08x\n", what, v[0], v[1]);
+            (void)hipMemset(f, 0, 8);
+        }
+    }
     std::fflush(stderr);
 }
 
@@ -643,11 +666,6 @@ int run_pipeline(tsm_adc* h, Workspace* w, int K, const PairIn& in, size_t step,
     if (keep_view1 && (rc = dump_vol(dump->cost_scan, 2)) != TSM_OK) return rc;
     if (dump && dump->wta && (rc = d2h(dump->wta, w->rb.disp0, 2 * N * 4)) != TSM_OK) return rc;
     // --- refinement --------------------------------------------------------------------
-#ifdef TSM_EXP_NO_REFINE  // timing probe (make exp): what the refinement chain costs a group
-    mark_stage();
-    if (h->profiling) w->pending.emplace_back(ev, K);
-    return TSM_OK;
-#endif
     launch_outlier(w->rb, P, st);
     if (dump && dump->outlier && (rc = d2h(dump->outlier, w->rb.dm, N * 4)) != TSM_OK) return rc;
     {

@@ -17,9 +17,6 @@
 
 namespace tsm {
 
-#define TSM_STR2(x) #x
-#define TSM_STR(x) TSM_STR2(x)
-
 // computeLimit, ADCensus.cpp:604-659 (returns the arm length; one shorter when the walk
 // ends at the image border, :650-658).  p: the pixel; fetch(k): the pixel k steps along the
 // arm's direction; avail: how many such steps stay inside the image.  The walk loads
@@ -235,6 +232,7 @@ struct AggStream {
     int cpl;               // chunks per line
     int nlv;               // lines per view
     int nl;                // lines of both views
+    uint32_t* err;         // CHK: the trace flag (trace_flag())
 };
 
 constexpr int AX_MIR = 3;  // mirror slots after each ring (a 4-read block spans 3 slots past its start)
@@ -282,7 +280,11 @@ static_assert(AS_RP1 == AS_RP2, "pass B's ring2 window starts at pass A's ring1 
 //   [1] window length, 0 = no output (past the line or the workgroup's stream)
 //   [2] RN(1/windowSize) bits   [3] windowSize as float
 //   [4] the pixel's volume byte offset from the slice base, low word   [5] high word
-template <bool FUSED, int QT, bool BIG>
+//
+// CHK (TSM_TRACE builds of a launch): every descriptor a wave consumes is range-checked
+// (ring offset inside its ring and on a pixel slot, window length within the rings' reach,
+// volume offset inside the slice); a bad one sets the trace flag and its step does nothing.
+template <bool FUSED, int QT, bool BIG, bool CHK = false>
 __global__ __launch_bounds__(AX_THREADS) void k_agg_split(AggStream S, DevParams Pk) {
     const DevParams P = Pk;
     pair_shift(blockIdx.z, P.pstride, S.vol, S.arms, S.ws, S.pk, S.rcp);
@@ -317,17 +319,23 @@ __global__ __launch_bounds__(AX_THREADS) void k_agg_split(AggStream S, DevParams
     const int nblk = (nsteps + AX_D - 1) / AX_D;  // every wave runs nblk * AX_D steps
     const uint32_t lane16 = (uint32_t)lane * 16;
     const bool vl = lane < Q;
-#ifdef TSM_EXP_AGG_SALU  // timing probe (make exp): TSM_EXP_AGG_SALU extra scalar adds a step and wave
-    auto barrier = [&]() {
-        uint32_t d;
-        asm volatile("s_mov_b32 %0, 0\n.rept " TSM_STR(TSM_EXP_AGG_SALU) "\ns_add_u32 %0, %0, 1\n.endr" : "=s"(d));
-        asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+    // CHK: descriptor ranges (see above); kind 1 = pass-A window, 2 = pass-B window, 3 = store
+    const size_t vol_bytes = 2 * vstride * 4 - (size_t)16 * slice * S.qn0;  // slice base to volume end
+    auto bad_desc = [&](uint32_t kind, uint32_t off, int len, uint32_t rb, uint32_t re) -> bool {
+        const bool bad = len < 0 || len > 2 * AS_MAX_ARM + 1 ||
+                         (len > 0 && (off < rb || off >= re || (off - rb) % Qs != 0));
+        if (bad && lane == 0) { S.err[1] = off; S.err[0] = kind; }
+        return bad;
     };
-#elif defined(TSM_EXP_AGG_NOBARRIER)  // timing probe (make exp): no per-step barrier (wrong results)
-    auto barrier = [&]() { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); };
-#else
+    auto bad_store = [&](uint32_t lo, uint32_t hi) -> bool {
+        const size_t o = BIG ? ((size_t)hi << 32 | lo) : (size_t)lo;
+        const bool bad = (o & 15) != 0 || o + (size_t)Q * 16 > vol_bytes;
+        if (bad && lane == 0) { S.err[1] = lo; S.err[0] = 3u; }
+        return bad;
+    };
+    // the step's barrier is the descriptor protocol: a descriptor is read only after the
+    // barrier that follows its write (a probe without it faulted, round 4)
     auto barrier = [&]() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); };
-#endif
     // sequential window sum of `len` ring pixels from LDS byte offset `off` (a slot of the
     // ring [rb, re)): whole blocks of 4 at immediate offsets (the mirror slots make every
     // block contiguous), then the 1-3 remaining pixels under uniform branches -- the
@@ -439,11 +447,7 @@ __global__ __launch_bounds__(AX_THREADS) void k_agg_split(AggStream S, DevParams
                 rv[k] = *reinterpret_cast<const f32x4*>(volq + o + 4 * lanec);
             } else {
                 // single passes (the first and the last) load with the streaming policy (kNtLoad)
-#ifdef TSM_EXP_AGG_NOLOAD  // timing probe: every A wave re-reads one L2-resident vector
-                rv[k] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rs_vol, voff, lo & 0xffffu, 0));
-#else
                 rv[k] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rs_vol, voff, lo, FUSED ? 0 : kNtLoad));
-#endif
             }
         };
         auto land = [&](const f32x4& val, int ci) {  // pixel w of a chunk -> ring1 slot index ci
@@ -483,17 +487,14 @@ __global__ __launch_bounds__(AX_THREADS) void k_agg_split(AggStream S, DevParams
                 land(rv[u], (u + AS_AHEAD) % AX_D);
                 issue(u, cur, u);
                 const uint32_t a_off = __builtin_amdgcn_readfirstlane(mA.x);
-                const int a_len = (int)__builtin_amdgcn_readfirstlane(mA.y);
+                int a_len = (int)__builtin_amdgcn_readfirstlane(mA.y);
+                if constexpr (CHK) if (bad_desc(1u, a_off, a_len, r1_off, r1_end)) a_len = 0;
                 const float a_y = __uint_as_float(__builtin_amdgcn_readfirstlane(mA.z));
                 const float a_b = __uint_as_float(__builtin_amdgcn_readfirstlane(mA.w));
                 mA = *reinterpret_cast<const u32x4*>(mbase + mslot(par, u + 1));  // chunk s + 1
                 const uint32_t r2w = r2_off + (uint32_t)(u * AS_SEG + w) * Qs;  // ring2 slot of chunk s
                 if (a_len) {
-#ifdef TSM_EXP_AGG_WIN1  // timing probe: one-pixel windows in pass A and pass B
-                    f32x4 acc = window(a_off, 1, r1_off, r1_end);
-#else
                     f32x4 acc = window(a_off, a_len, r1_off, r1_end);
-#endif
                     if (S.ws) acc = div_ws(acc, a_b, a_y);
                     if (vl) {
                         *reinterpret_cast<f32x4*>(lds + r2w + lane16) = acc;
@@ -521,25 +522,21 @@ __global__ __launch_bounds__(AX_THREADS) void k_agg_split(AggStream S, DevParams
             const int s = b * AX_D + u;
             const int ub = (u - lag + 2 * AX_D) % AX_D;  // ring chunk slot of chunk s - lag
             const uint32_t b_off = __builtin_amdgcn_readfirstlane(mB.x) + d21;
-            const int b_len = (int)__builtin_amdgcn_readfirstlane(mB.y);
+            int b_len = (int)__builtin_amdgcn_readfirstlane(mB.y);
             const uint32_t olo = __builtin_amdgcn_readfirstlane(mO.x);
             const uint32_t ohi = BIG ? __builtin_amdgcn_readfirstlane(mO.y) : 0u;
+            if constexpr (CHK) {
+                if (s >= lag && b_len && ((FUSED && bad_desc(2u, b_off, b_len, r2_off, r2_end)) || bad_store(olo, ohi)))
+                    b_len = 0;
+            }
             const char* mn = mbase + mslot(par, u - lag + 1);  // chunk s - lag + 1
             mB = *reinterpret_cast<const u32x2*>(mn);
             mO = *reinterpret_cast<const u32x2*>(mn + 16);
             const uint32_t r2r = r2_off + (uint32_t)(ub * AS_SEG + w) * Qs;  // single: chunk s - 1
             if (s >= lag && b_len) {
-#ifdef TSM_EXP_AGG_WIN1
-                const f32x4 acc = FUSED ? window(b_off, 1, r2_off, r2_end)
-#else
                 const f32x4 acc = FUSED ? window(b_off, b_len, r2_off, r2_end)
-#endif
                                         : *reinterpret_cast<const f32x4*>(lds + r2r + lane16);
-#ifdef TSM_EXP_AGG_NOSTORE  // timing probe: B waves compute but do not store
-                if (acc.x == -1.f) store(olo, ohi, acc);
-#else
                 store(olo, ohi, acc);
-#endif
             }
             barrier();
         }
@@ -602,6 +599,11 @@ constexpr size_t kLdsBytes = 160 * 1024;
 
 template <bool FUSED, int QT, bool BIG>
 static void launch_split_t(const AggStream& S, const DevParams& P, dim3 grid, size_t lds, hipStream_t st) {
+    if (S.err) {  // TSM_TRACE: the descriptor-checked variant (generic label count)
+        ensure_lds_limit((const void*)k_agg_split<FUSED, 0, BIG, true>, kLdsBytes);
+        hipLaunchKernelGGL((k_agg_split<FUSED, 0, BIG, true>), grid, dim3(AX_THREADS), lds, st, S, P);
+        return;
+    }
     ensure_lds_limit((const void*)k_agg_split<FUSED, QT, BIG>, kLdsBytes);
     hipLaunchKernelGGL((k_agg_split<FUSED, QT, BIG>), grid, dim3(AX_THREADS), lds, st, S, P);
 }
@@ -648,6 +650,7 @@ int launch_aggregation_pass(float* vol, const uint32_t* arms, const int32_t* ws,
     S.cpl = (S.n + AS_SEG - 1) / AS_SEG;
     S.nlv = horizontal ? P.H : P.W;
     S.nl = 2 * S.nlv;
+    S.err = trace_flag();
     const int ncu = P.ncu;
     const int G = S.nl < ncu ? S.nl : ncu;
     // every pass through the role-split streamer (round 4, same box: 409 against 406.5

@@ -313,13 +313,6 @@ __global__ __launch_bounds__(CW_THREADS) __attribute__((amdgpu_waves_per_eu(E ==
     // or j0 + k (view 1), clamped: labels whose column leaves the image are border cells,
     // fixed up per step.  (Rotation 0: label offset e sits in slot e in both views.)
     uint32_t V[NW][E];
-#ifdef TSM_EXP_COST_NOWARM  // timing probe (make exp): no warm-up gather (garbage costs)
-#pragma unroll
-    for (int e = 0; e < E; ++e)
-#pragma unroll
-        for (int w = 0; w < NW; ++w) V[w][e] = (uint32_t)(lane * 3 + e + w);
-    if (false)
-#endif
 #pragma unroll
     for (int e = 0; e < E; ++e) {
         const int k = kb + E * lane + e;
@@ -352,11 +345,7 @@ __global__ __launch_bounds__(CW_THREADS) __attribute__((amdgpu_waves_per_eu(E ==
     // the pixel stores it beside the pixel's main store, so the two land in one L2 line
     // while it is still there (a tail stored after the walk reached HBM as separate partial
     // lines: 46 MB of the launch's 776 MB written, and re-fetched its records: round 3 PMC).
-#ifdef TSM_EXP_COST_NOWARM  // ... and no tail gather
-    if (false) {
-#else
     if (tail) {
-#endif
         if (lane < count) {
             const int j = x_lo + lane;
             const float inf = __int_as_float(0x7f800000);
@@ -493,11 +482,7 @@ __global__ __launch_bounds__(CW_THREADS) __attribute__((amdgpu_waves_per_eu(E ==
 #pragma unroll
             for (int e = 0; e < E; ++e) c[e] = kb + E * lane + e >= L ? kInf : c[e];
         }
-#ifdef TSM_EXP_COST_NOSTORE  // timing probe (make exp): the walk without its volume stores
-        if ((fast || t < count) && c[0] == -1.f) {
-#else
         if (fast || t < count) {
-#endif
             if constexpr (E == 3) {  // labels 3l .. 3l+2: one 12-B store per lane, 768 B a pixel
                 F3 o3;
                 o3.a = c[0];

@@ -110,6 +110,7 @@ __device__ __forceinline__ void block_scan2(int& a, int& b, int* sa, int* sb) {
 
 
 constexpr int VD_THREADS = 512;  // the vote decision: threads a high-vote outlier
+constexpr size_t kVdStaticLds = (size_t)VD_THREADS * 2 * sizeof(uint32_t);  // its static rank list
 constexpr int RI_B = 4;          // interpolation rays: steps loaded a round trip
 constexpr int RW_B = 8;          // region walks: row-segment pixels loaded a round trip (minD >= 0,
                                  // so -1 marks a slot past the segment)
@@ -312,7 +313,7 @@ __global__ __launch_bounds__(VD_THREADS) void k_vote_decide_rank(
     // workgroup b takes bits [8q, 8q + 8) (q = b mod 4) of the words b / 4 + k G4: clustered
     // high-vote outliers (tens to a word) are spread over four workgroups.  Its words are
     // read in one round trip (a thread each) and the non-empty ones listed in LDS.
-    __shared__ uint32_t s_list[VD_THREADS][2];
+    __shared__ uint32_t s_list[VD_THREADS][2];  // kVdStaticLds bytes
     __shared__ int s_n;
     const int q = blockIdx.x & 3, G4 = gridDim.x >> 2, w0 = blockIdx.x >> 2;
     const int nk = w0 < nwords ? (nwords - w0 + G4 - 1) / G4 : 0;
@@ -934,8 +935,10 @@ void launch_region_voting(RefineBufs& B, const uint32_t* arms0, int hf, const De
     // grid-stride over quarter words of the bitmap, one round of resident workgroups (a
     // workgroup per quarter word of a full image's ranks measured 32 us a launch, most idle)
     const size_t lds = (size_t)8 * P.L * sizeof(int);  // a histogram per rank of a quarter word
+    // the attribute covers dynamic LDS only; with the static rank list it must fit the CU
+    static_assert(8 * 2048 * sizeof(int) + kVdStaticLds <= 160 * 1024, "vote-decision LDS past 160 KB");
     const int vd_blocks = 4 * std::max(16, 256 / std::max(1, P.npairs));
-    ensure_lds_limit((const void*)k_vote_decide_rank, lds + 4096);  // + its static rank list
+    ensure_lds_limit((const void*)k_vote_decide_rank, lds);
     hipLaunchKernelGGL(k_vote_decide_rank, grid1d(vd_blocks, P), dim3(VD_THREADS), lds, st, B.dm, B.dtmp,
                        arms0, B.out_list, B.cvote, B.csamp, B.counts, B.vbits, nb, hf, P);
     trace_point("k_vote_decide_rank", st);

@@ -196,11 +196,7 @@ __device__ __forceinline__ void scan_issue(StepIn<J>& s, int pos, int dir, int l
                                            const ScanConst& C) {
     const int pm = dir > 0 ? pos : pos + 1;  // max(pos, predecessor)
 #pragma unroll
-#ifdef TSM_EXP_SCAN_NTLOAD  // probe: streaming loads of the pixel vectors
-    for (int j = 0; j < J; ++j) s.p[j] = __builtin_nontemporal_load(reinterpret_cast<const f32x4*>(pv[j]));
-#else
     for (int j = 0; j < J; ++j) s.p[j] = *reinterpret_cast<const f32x4*>(pv[j]);  // (nt loads: -2 %)
-#endif
     const uint32_t i1 = (uint32_t)(HORIZ ? C.gpad + pm : pm * C.gstride + C.gpad + line);
     // d1 as the aligned dword holding its byte (a byte load's value is narrowed by the
     // compiler, which then re-widens every ring slot at the loop back-edge, waiting for it)
@@ -618,11 +614,7 @@ static int launch_scan(float* vol, const uint8_t* grad, const uint32_t* img, int
             else launch_scan_m<1, 8, HORIZ, WTA>(vol, grad, img, dir, wta, store_view1, infvec, P, st);
         } else {
             (void)deep;
-#ifdef TSM_EXP_SCAN_VK16  // probe: 16 steps in flight in the vertical passes
-            launch_scan_m<1, 16, HORIZ, WTA>(vol, grad, img, dir, wta, store_view1, infvec, P, st);
-#else
             launch_scan_m<1, 8, HORIZ, WTA>(vol, grad, img, dir, wta, store_view1, infvec, P, st);
-#endif
         }
     } else if (J == 2) {
         launch_scan_m<2, 8, HORIZ, WTA>(vol, grad, img, dir, wta, store_view1, infvec, P, st);

@@ -86,9 +86,6 @@ __device__ __forceinline__ f32x4 div_ws(f32x4 a, float b, float y) {
 // fetched once into that XCD's L2 instead of once by each of two XCDs.  A permutation of
 // [0, n); blocks past the last multiple of 8 keep their index.
 __device__ __forceinline__ int xcd_remap(int b, int n) {
-#ifdef TSM_EXP_NO_XCD_REMAP  // timing probe (make exp): the plain block order
-    return b;
-#endif
     const int per = n >> 3;
     return b < 8 * per ? (b & 7) * per + (b >> 3) : b;
 }

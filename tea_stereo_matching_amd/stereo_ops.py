@@ -56,10 +56,12 @@ def _f32(a):
     if _is_dev(a):
         import torch
 
-        assert a.dtype == torch.float32 and a.dim() == 2, "expected a 2-D float32 tensor"
+        if a.dtype != torch.float32 or a.dim() != 2:
+            raise ValueError(f"expected a 2-D float32 tensor, got {a.dtype} with {a.dim()} dims")
         return a.contiguous()
     a = np.ascontiguousarray(a, dtype=np.float32)
-    assert a.ndim == 2, "expected a 2-D float32 map"
+    if a.ndim != 2:
+        raise ValueError(f"expected a 2-D float32 map, got {a.ndim} dims")
     return a
 
 
@@ -150,8 +152,10 @@ def _write_cloud(fn: str, RGBImage, XYZPoints, path: str) -> None:
     xyz = np.ascontiguousarray(np.asarray(XYZPoints, dtype=np.float32))
     if img.size == 0 or xyz.size == 0 or not path:
         return  # the reference logs "Empty input." and returns (stereo.cpp:252-256)
+    if xyz.ndim != 3 or xyz.shape[2] != 3 or img.ndim != 3 or img.shape != xyz.shape[:2] + (3,):
+        raise ValueError(f"{fn}: expected H x W x 3 BGR image and points of one size, got "
+                         f"{img.shape} and {xyz.shape}")
     H, W = xyz.shape[:2]
-    assert img.shape[:2] == (H, W) and img.shape[2] == 3 and xyz.shape[2] == 3
     rc = getattr(N.load(), fn)(_ptr(img), 3 * W, _ptr(xyz), 12 * W, H, W, path.encode())
     _check(rc, fn)
 
@@ -221,6 +225,9 @@ def applyColorMapBatch(disparities, *args):
     applyColorMap; returns a list of (H, W, 3) uint8 tensors."""
     import torch
 
+    if len(args) == 3 and (_is_dev(args[0]) or isinstance(args[0], np.ndarray)) and np.ndim(args[2]) == 0:
+        # the round-3 form (disparities, colorMap, minVal, maxVal): refuse it by name
+        raise TypeError("applyColorMapBatch takes applyColorMap's order: (disparities, minVal, maxVal, colorMap)")
     if len(args) == 0:
         cmap, use_range, mn, mx = JETColorMap(), 0, 0.0, 0.0
     elif len(args) == 1:

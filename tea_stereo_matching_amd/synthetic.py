@@ -108,6 +108,23 @@ def config_b(seed: int = 1000):
     return make_scene(seed, 375, 1242, 193)
 
 
+def add_noise(img: np.ndarray, seed: int, amp: int = 3, stream: int = 7000) -> np.ndarray:
+    """img + independent integer noise U[-amp, amp] per pixel and channel (splitmix64 of
+    (seed, stream, index)), clamped to u8.  Added to one view only, it breaks the exact
+    shift of the synthetic pairs, so no aggregated cost at the true disparity is exactly 0
+    -- the property of real pairs that decides how many vectors the scanline stores
+    (ADCensus.cpp:880-881 leaves a pixel untouched when its predecessor's minimum is 0)."""
+    idx = np.arange(img.size, dtype=np.uint64)
+    n = _uniform_int(seed, stream, idx, -amp, amp).reshape(img.shape)
+    return np.clip(img.astype(np.int64) + n, 0, 255).astype(np.uint8)
+
+
+def config_b_noisy(seed: int = 1000, amp: int = 3):
+    """config B pair `seed` with independent +-amp noise on the right view (bench B_noisy)."""
+    left, right, gt = config_b(seed)
+    return left, add_noise(right, seed, amp), gt
+
+
 def config_c(seed: int = 2000):
     """1500x1000, setMinMaxDisparity(0, 256) -> 257 labels."""
     return make_scene(seed, 1000, 1500, 257)

@@ -23,6 +23,12 @@ Cases:
   B_HSI_1000     config B pair 1000 in the reference's default HSI model (bench configs block)
   B_OMP20_1000   config B pair 1000, RGB, with the racy-schedule emulation at T = 20 (the
                  mode equal to the reference's shipped outputs; bench configs block)
+  A_0600         demo-imgs/0600 (1280x720), setMinMaxDisparity(0, 192), RGB, serial scanline
+                 (BASELINE configs[0], timed in the bench's configs block)
+  A_0600_OMP20   the same with the T = 20 emulation: the disparity behind the reference's
+                 shipped demo-output/0600_adcensus.png
+  B_NOISY_<s>    config B pair s with independent +-3 noise on the right view
+                 (synthetic.config_b_noisy): no exact-zero aggregated minima
 
     python tests/golden/make_config_hashes.py [--threads N] [--only C B_1000 ...]
 """
@@ -74,6 +80,12 @@ def cases():
         out.append((f"B_{s}", (lambda s=s: syn.config_b(s)), 192, rgb))
     out.append(("B_HSI_1000", lambda: syn.config_b(1000), 192, {"color_model": O.HSI}))
     out.append(("B_OMP20_1000", lambda: syn.config_b(1000), 192, dict(rgb, scan_emulate_threads=20)))
+    # the bench's real-image and noisy entries (BASELINE configs[0] and the data-dependence
+    # check of the scanline's skipped stores)
+    out.append(("A_0600", _demo_0600, 192, rgb))
+    out.append(("A_0600_OMP20", _demo_0600, 192, dict(rgb, scan_emulate_threads=20)))
+    for s in (1000, 1063, 1064, 1127):
+        out.append((f"B_NOISY_{s}", (lambda s=s: syn.config_b_noisy(s)), 192, rgb))
     return out
 
 

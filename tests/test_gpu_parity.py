@@ -401,9 +401,11 @@ def test_config_b_modes_full_size(matcher, tsm, key, model, omp):
 
     gold = json.load(open(os.path.join(GOLDEN, "config_hashes.json")))[key]
     left, right, _ = tsm.synthetic.config_b(1000)
-    d_g, _ = _gpu(matcher, tsm, left, right, model, 0, 192, omp=omp)
-    matcher.setOmpEmulation(0)
-    matcher.setMatchingStrategy(tsm.ColorModel.RGB)
+    try:
+        d_g, _ = _gpu(matcher, tsm, left, right, model, 0, 192, omp=omp)
+    finally:  # the shared matcher goes back to the serial RGB mode even on failure
+        matcher.setOmpEmulation(0)
+        matcher.setMatchingStrategy(tsm.ColorModel.RGB)
     d_g = np.ascontiguousarray(d_g, dtype=np.float32)
     assert hashlib.sha256(d_g.tobytes()).hexdigest() == gold["sha256"]
 
@@ -465,12 +467,13 @@ def test_reference_fixture_0045_exact(matcher, tsm, oracle, demo_pair_0045):
     assert np.array_equal(col, ref), f"{(col != ref).any(-1).sum()} pixels differ"
 
 
-@pytest.mark.parametrize("case", ["MOTO", "ROI_0600", "MASK_HSI_0600"])
+@pytest.mark.parametrize("case", ["MOTO", "ROI_0600", "MASK_HSI_0600", "A_0600", "A_0600_OMP20"])
 def test_real_pairs_full_size(matcher, tsm, demo_pair_0600, case):
     """The reference's real demo pairs at full size against oracle hashes
     (tests/golden/make_config_hashes.py): the Middlebury Motorcycle pair of config C
     (1482x994, D=[0,256]); 0600 (1280x720) in ROI mode (maxD := W/2 = 640, 641 labels) and in
-    mask mode with the reference's default HSI model."""
+    mask mode with the reference's default HSI model; 0600 at D=[0,192] serial and with the
+    T = 20 race emulation (BASELINE configs[0], the bench's A_real entries)."""
     import hashlib
     import json
 
@@ -483,10 +486,29 @@ def test_real_pairs_full_size(matcher, tsm, demo_pair_0600, case):
     else:
         left, right = demo_pair_0600
     model = gold.get("color_model", 0)
-    d_g, _ = _gpu(matcher, tsm, left, right, model, 0, gold["max_disparity"],
-                  roi=bool(gold.get("roi_matching", 0)), mask=bool(gold.get("mask_matching", 0)))
-    matcher.setMatchingStrategy(tsm.ColorModel.RGB)
+    try:
+        d_g, _ = _gpu(matcher, tsm, left, right, model, 0, gold["max_disparity"],
+                      roi=bool(gold.get("roi_matching", 0)), mask=bool(gold.get("mask_matching", 0)),
+                      omp=gold.get("scan_emulate_threads", 0))
+    finally:
+        matcher.setOmpEmulation(0)
+        matcher.setMatchingStrategy(tsm.ColorModel.RGB)
     d_g = np.ascontiguousarray(d_g, dtype=np.float32)
     assert list(d_g.shape) == gold["shape"]
     assert abs(float((d_g >= 0).mean()) - gold["valid_fraction"]) < 1e-12
+    assert hashlib.sha256(d_g.tobytes()).hexdigest() == gold["sha256"]
+
+
+@pytest.mark.parametrize("seed", [1000, 1127])
+def test_config_b_noisy_full_size(matcher, tsm, seed):
+    """Config B with independent +-3 noise on the right view (synthetic.config_b_noisy, the
+    bench's B_noisy entry): no exact-zero aggregated minima, so the scanline updates and
+    stores every vector.  SHA-256 of the fp32 disparity == the oracle's."""
+    import hashlib
+    import json
+
+    gold = json.load(open(os.path.join(GOLDEN, "config_hashes.json")))[f"B_NOISY_{seed}"]
+    left, right, _ = tsm.synthetic.config_b_noisy(seed)
+    d_g, _ = _gpu(matcher, tsm, left, right, 0, 0, 192)
+    d_g = np.ascontiguousarray(d_g, dtype=np.float32)
     assert hashlib.sha256(d_g.tobytes()).hexdigest() == gold["sha256"]
