@@ -327,7 +327,8 @@ void layout_slot(Workspace* w, SlotLayout& S, int H, int W, int L, int model) {
     S.take(B.cvote, N * 4);
     S.take(B.csamp, N * 20 * 2);
     S.take(B.bsum, 2 * refine_scan_blocks((int)N) * 4 + 64);
-    S.take(B.vbits, refine_vote_bits_bytes((int)N));
+    S.take(B.hv_list, N * 4);
+    S.take(B.long_list, N * 4);
     S.take(B.counts, 16);
     S.take(B.gray, N);
     S.take(B.gray_eq, N);
@@ -341,6 +342,7 @@ void layout_slot(Workspace* w, SlotLayout& S, int H, int W, int L, int model) {
     S.take(B.strong, N);
     S.take(B.edges, N);
     S.take(B.subpix, N * 4);
+    S.take(B.vpre, refine_vpre_ints(H, W) * 4);
 }
 
 // Bytes of one pair slot (the per-pair part of a workspace arena), as ensure_workspace

@@ -321,9 +321,12 @@ __global__ __launch_bounds__(AX_THREADS) void k_agg_split(AggStream S, DevParams
     const bool vl = lane < Q;
     // CHK: descriptor ranges (see above); kind 1 = pass-A window, 2 = pass-B window, 3 = store
     const size_t vol_bytes = 2 * vstride * 4 - (size_t)16 * slice * S.qn0;  // slice base to volume end
-    auto bad_desc = [&](uint32_t kind, uint32_t off, int len, uint32_t rb, uint32_t re) -> bool {
-        const bool bad = len < 0 || len > 2 * AS_MAX_ARM + 1 ||
-                         (len > 0 && (off < rb || off >= re || (off - rb) % Qs != 0));
+    // lw = len | n1 << 16: n1 <= len, and the first piece ends inside the ring (or at its end)
+    auto bad_desc = [&](uint32_t kind, uint32_t off, uint32_t lw, uint32_t rb, uint32_t re) -> bool {
+        const uint32_t len = lw & 0xffffu, n1 = lw >> 16;
+        const bool bad = len > 2 * AS_MAX_ARM + 1 || n1 > len ||
+                         (len > 0 && (off < rb || off >= re || (off - rb) % Qs != 0 ||
+                                      off + n1 * Qs > re || (n1 < len && off + n1 * Qs != re)));
         if (bad && lane == 0) { S.err[1] = off; S.err[0] = kind; }
         return bad;
     };
@@ -341,13 +344,12 @@ __global__ __launch_bounds__(AX_THREADS) void k_agg_split(AggStream S, DevParams
     // block contiguous), then the 1-3 remaining pixels under uniform branches -- the
     // reference's order, no padding reads.  The running offset is a VGPR (its wrap a
     // v_cndmask): only the block count is scalar.
-    auto window = [&](uint32_t off, int len, uint32_t rb, uint32_t re) -> f32x4 {
-        f32x4 acc = f32x4{0.f, 0.f, 0.f, 0.f};
-        uint32_t vo = off;
-        asm volatile("" : "+v"(vo));  // a vector value from here on
-        const uint32_t span = re - rb;
-        for (int nb = len >> 2; nb > 0; --nb) {
-            const char* p = lds + vo + lane16;
+    // The descriptor also holds n1, the elements before the ring's end (len | n1 << 16), so
+    // the window runs as two straight pieces -- n1 elements from off, the rest from the
+    // ring's start -- with no per-block wrap test: per block of 4 elements one address add.
+    auto piece = [&](f32x4& acc, uint32_t off, int n) {
+        const char* p = lds + off + lane16;
+        for (int nb = n >> 2; nb > 0; --nb) {
             const f32x4 x0 = *reinterpret_cast<const f32x4*>(p);
             const f32x4 x1 = *reinterpret_cast<const f32x4*>(p + Qs);
             const f32x4 x2 = *reinterpret_cast<const f32x4*>(p + 2 * Qs);
@@ -356,12 +358,10 @@ __global__ __launch_bounds__(AX_THREADS) void k_agg_split(AggStream S, DevParams
             acc += x1;
             acc += x2;
             acc += x3;
-            vo += 4 * Qs;
-            vo = vo >= re ? vo - span : vo;
+            p += 4 * Qs;
         }
-        const int r = len & 3;
-        if (r) {
-            const char* p = lds + vo + lane16;
+        const int r = n & 3;
+        if (r) {  // the mirror slots keep a block starting at the ring's last slot in range
             const f32x4 x0 = *reinterpret_cast<const f32x4*>(p);
             const f32x4 x1 = *reinterpret_cast<const f32x4*>(p + Qs);
             const f32x4 x2 = *reinterpret_cast<const f32x4*>(p + 2 * Qs);
@@ -369,6 +369,13 @@ __global__ __launch_bounds__(AX_THREADS) void k_agg_split(AggStream S, DevParams
             if (r > 1) acc += x1;
             if (r > 2) acc += x2;
         }
+    };
+    auto window = [&](uint32_t off, uint32_t lw, uint32_t rb, uint32_t re) -> f32x4 {
+        (void)re;
+        f32x4 acc = f32x4{0.f, 0.f, 0.f, 0.f};
+        const int len = (int)(lw & 0xffffu), n1 = (int)(lw >> 16);
+        piece(acc, off, n1);
+        if (len > n1) piece(acc, rb, len - n1);
         return acc;
     };
     const uint32_t mstep = AS_SEG * AX_MW * 4;
@@ -432,8 +439,9 @@ __global__ __launch_bounds__(AX_THREADS) void k_agg_split(AggStream S, DevParams
                 int st = slot - lo;
                 st = st < 0 ? st + AS_RP1 : st;
                 const uint32_t len = Bt.valid ? (uint32_t)(lo + hi + 1) : 0u;
+                const uint32_t n1 = min(len, (uint32_t)(AS_RP1 - st));  // elements before the ring end
                 char* m = lds + meta_off + (uint32_t)(((m0 + lane) % AX_MC) * AS_SEG + w) * AX_MW * 4;
-                *reinterpret_cast<u32x4*>(m) = u32x4{r1_off + (uint32_t)st * Qs, len, Bt.my,
+                *reinterpret_cast<u32x4*>(m) = u32x4{r1_off + (uint32_t)st * Qs, len | n1 << 16, Bt.my,
                                                      __float_as_uint((float)(int)(Bt.ma >> 16))};
                 *reinterpret_cast<u32x2*>(m + 16) = u32x2{Bt.olo, Bt.ohi};
             }
@@ -487,14 +495,15 @@ __global__ __launch_bounds__(AX_THREADS) void k_agg_split(AggStream S, DevParams
                 land(rv[u], (u + AS_AHEAD) % AX_D);
                 issue(u, cur, u);
                 const uint32_t a_off = __builtin_amdgcn_readfirstlane(mA.x);
-                int a_len = (int)__builtin_amdgcn_readfirstlane(mA.y);
-                if constexpr (CHK) if (bad_desc(1u, a_off, a_len, r1_off, r1_end)) a_len = 0;
+                uint32_t a_lw = __builtin_amdgcn_readfirstlane(mA.y);
+                if constexpr (CHK) if (bad_desc(1u, a_off, a_lw, r1_off, r1_end)) a_lw = 0;
+                const int a_len = (int)(a_lw & 0xffffu);
                 const float a_y = __uint_as_float(__builtin_amdgcn_readfirstlane(mA.z));
                 const float a_b = __uint_as_float(__builtin_amdgcn_readfirstlane(mA.w));
                 mA = *reinterpret_cast<const u32x4*>(mbase + mslot(par, u + 1));  // chunk s + 1
                 const uint32_t r2w = r2_off + (uint32_t)(u * AS_SEG + w) * Qs;  // ring2 slot of chunk s
                 if (a_len) {
-                    f32x4 acc = window(a_off, a_len, r1_off, r1_end);
+                    f32x4 acc = window(a_off, a_lw, r1_off, r1_end);
                     if (S.ws) acc = div_ws(acc, a_b, a_y);
                     if (vl) {
                         *reinterpret_cast<f32x4*>(lds + r2w + lane16) = acc;
@@ -522,19 +531,20 @@ __global__ __launch_bounds__(AX_THREADS) void k_agg_split(AggStream S, DevParams
             const int s = b * AX_D + u;
             const int ub = (u - lag + 2 * AX_D) % AX_D;  // ring chunk slot of chunk s - lag
             const uint32_t b_off = __builtin_amdgcn_readfirstlane(mB.x) + d21;
-            int b_len = (int)__builtin_amdgcn_readfirstlane(mB.y);
+            uint32_t b_lw = __builtin_amdgcn_readfirstlane(mB.y);
             const uint32_t olo = __builtin_amdgcn_readfirstlane(mO.x);
             const uint32_t ohi = BIG ? __builtin_amdgcn_readfirstlane(mO.y) : 0u;
             if constexpr (CHK) {
-                if (s >= lag && b_len && ((FUSED && bad_desc(2u, b_off, b_len, r2_off, r2_end)) || bad_store(olo, ohi)))
-                    b_len = 0;
+                if (s >= lag && b_lw && ((FUSED && bad_desc(2u, b_off, b_lw, r2_off, r2_end)) || bad_store(olo, ohi)))
+                    b_lw = 0;
             }
+            const int b_len = (int)(b_lw & 0xffffu);
             const char* mn = mbase + mslot(par, u - lag + 1);  // chunk s - lag + 1
             mB = *reinterpret_cast<const u32x2*>(mn);
             mO = *reinterpret_cast<const u32x2*>(mn + 16);
             const uint32_t r2r = r2_off + (uint32_t)(ub * AS_SEG + w) * Qs;  // single: chunk s - 1
             if (s >= lag && b_len) {
-                const f32x4 acc = FUSED ? window(b_off, b_len, r2_off, r2_end)
+                const f32x4 acc = FUSED ? window(b_off, b_lw, r2_off, r2_end)
                                         : *reinterpret_cast<const f32x4*>(lds + r2r + lane16);
                 store(olo, ohi, acc);
             }

@@ -109,8 +109,6 @@ __device__ __forceinline__ void block_scan2(int& a, int& b, int* sa, int* sb) {
 }
 
 
-constexpr int VD_THREADS = 512;  // the vote decision: threads a high-vote outlier
-constexpr size_t kVdStaticLds = (size_t)VD_THREADS * 2 * sizeof(uint32_t);  // its static rank list
 constexpr int RI_B = 4;          // interpolation rays: steps loaded a round trip
 constexpr int RW_B = 8;          // region walks: row-segment pixels loaded a round trip (minD >= 0,
                                  // so -1 marks a slot past the segment)
@@ -143,20 +141,14 @@ __global__ void k_oscan_count(const int32_t* __restrict__ disp, int n, int minD,
 }
 
 // out_list[rank] = pixel of each outlier; dtmp = disp everywhere (the Jacobi output
-// starts as the input; the decision overwrites high-vote outliers)
-// High-vote rank bitmaps (filled by the vote count, read by the decision): level 0 holds one
-// bit per rank, level 1 one bit per level-0 word; a block of SC_BLOCK pixels clears the
-// words its ranks can reach (ranks < pixels).
-constexpr int VB_L0 = SC_BLOCK / 32, VB_L1 = SC_BLOCK / 1024;  // words per scan block
-__host__ __device__ inline size_t vote_bits_words(int nb) { return (size_t)nb * (VB_L0 + VB_L1); }
-
+// starts as the input; the decision overwrites high-vote outliers).
 // Each block's first rank is the sum of the outlier counts of the blocks before it (read
 // and reduced here: a few hundred counts, no separate scan launch); the last block writes
 // the total.
 __global__ void k_oscan_scatter(const int32_t* __restrict__ disp, int n, int minD, const int32_t* __restrict__ bsum,
                                 int32_t* __restrict__ out_list, int32_t* __restrict__ dtmp,
-                                uint32_t* __restrict__ vbits, int32_t* __restrict__ counts, size_t ps) {
-    pair_shift(blockIdx.z, ps, disp, bsum, out_list, dtmp, vbits, counts);
+                                int32_t* __restrict__ counts, size_t ps) {
+    pair_shift(blockIdx.z, ps, disp, bsum, out_list, dtmp, counts);
     __shared__ int s_base;
     if (threadIdx.x == 0) s_base = 0;
     __syncthreads();
@@ -165,8 +157,6 @@ __global__ void k_oscan_scatter(const int32_t* __restrict__ disp, int n, int min
         for (int i = threadIdx.x; i < (int)blockIdx.x; i += SC_THREADS) part += bsum[2 * i];
         if (part) atomicAdd(&s_base, part);
     }
-    if (threadIdx.x < VB_L0) vbits[blockIdx.x * VB_L0 + threadIdx.x] = 0u;
-    if (threadIdx.x < VB_L1) vbits[(size_t)gridDim.x * VB_L0 + blockIdx.x * VB_L1 + threadIdx.x] = 0u;
     __shared__ int sa[SC_THREADS], sb[SC_THREADS];
     const int base = blockIdx.x * SC_BLOCK + threadIdx.x * SC_ITEMS;
     int dv[SC_ITEMS];
@@ -180,6 +170,7 @@ __global__ void k_oscan_scatter(const int32_t* __restrict__ disp, int n, int min
     if (threadIdx.x == SC_THREADS - 1 && blockIdx.x == gridDim.x - 1) {
         counts[0] = first + sa[SC_THREADS - 1];
         counts[1] = 0;
+        counts[2] = 0;  // the decision's long-carry list (k_vote_decide_wave)
     }
     if (base + SC_ITEMS <= n) {
 #pragma unroll
@@ -193,6 +184,104 @@ __global__ void k_oscan_scatter(const int32_t* __restrict__ disp, int n, int min
         if (dv[k] < minD) out_list[a++] = base + k;
 }
 
+// Valid-pixel prefix counts along the inner direction of a voting pass (valid: disp >= minD,
+// the reference's sample test :1122): the vote of a row segment is then the difference of
+// two prefix entries, exact integer arithmetic in any order.
+//   rows (hf):     pre[y (W+1) + x] = valid pixels of row y at columns < x, x in [0, W]
+//   columns (!hf): P(y, x) = cpre[(y >> 5) W + x] + pre[y W + x], the valid pixels of column x
+//                  at rows < y (y in [0, H]): pre holds the count inside 32-row chunks, cpre
+//                  the counts of the chunks before (two launches, W x H/32 threads)
+constexpr int VP_CH = 32;
+size_t refine_vpre_ints(int H, int W) {
+    const size_t r = (size_t)H * (W + 1), c = (size_t)(H + 1) * W + (size_t)(H / VP_CH + 2) * W;
+    return r > c ? r : c;
+}
+
+__global__ __launch_bounds__(256) void k_vprefix_rows(const int32_t* __restrict__ disp, int32_t* __restrict__ pre,
+                                                      DevParams Pk) {
+    const DevParams P = Pk;
+    pair_shift(blockIdx.z, P.pstride, disp, pre);
+    __shared__ int s_w[4];
+    const int W = P.W, y = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+    const int32_t* row = disp + (size_t)y * W;
+    int32_t* out = pre + (size_t)y * (W + 1);
+    int carry = 0;
+    for (int x0 = 0; x0 < W; x0 += 256) {
+        const int x = x0 + tid;
+        const int v = x < W && row[x] >= P.minD ? 1 : 0;
+        int incl = v;
+#pragma unroll
+        for (int d = 1; d < 64; d <<= 1) {
+            const int t = __shfl_up(incl, d);
+            if (lane >= d) incl += t;
+        }
+        if (lane == 63) s_w[wv] = incl;
+        __syncthreads();
+        int before = carry;
+        for (int k = 0; k < wv; ++k) before += s_w[k];
+        if (x < W) out[x] = before + incl - v;
+        const int tot = s_w[0] + s_w[1] + s_w[2] + s_w[3];
+        __syncthreads();
+        carry += tot;
+    }
+    if (tid == 0) out[W] = carry;
+}
+
+// columns, step 1: thread (chunk c, column x) counts inside rows [32c, 32c + 32); the chunk
+// holding row H also writes P's local part at y = H
+__global__ __launch_bounds__(256) void k_vprefix_cols(const int32_t* __restrict__ disp, int32_t* __restrict__ pre,
+                                                      DevParams Pk) {
+    const DevParams P = Pk;
+    pair_shift(blockIdx.z, P.pstride, disp, pre);
+    const int W = P.W, H = P.H;
+    const int x = blockIdx.x * 256 + threadIdx.x, c = blockIdx.y;
+    if (x >= W) return;
+    int32_t* cpre = pre + (size_t)(H + 1) * W;
+    const int y0 = c * VP_CH, y1 = min(H, y0 + VP_CH);
+    int run = 0;
+    int dv[VP_CH];
+#pragma unroll
+    for (int k = 0; k < VP_CH; ++k) dv[k] = y0 + k < y1 ? disp[(size_t)(y0 + k) * W + x] : -1;
+#pragma unroll
+    for (int k = 0; k < VP_CH; ++k) {
+        if (y0 + k <= y1 && y0 + k <= H) {
+            if (y0 + k < H || (H - y0) < VP_CH) pre[(size_t)(y0 + k) * W + x] = run;
+        }
+        run += dv[k] >= P.minD ? 1 : 0;
+    }
+    cpre[(size_t)(c + 1) * W + x] = run;  // this chunk's total (scanned by step 2)
+}
+
+// columns, step 2: exclusive scan of the chunk totals per column (in place)
+__global__ __launch_bounds__(256) void k_vprefix_cols_scan(int32_t* __restrict__ pre, DevParams Pk) {
+    const DevParams P = Pk;
+    pair_shift(blockIdx.z, P.pstride, pre);
+    const int W = P.W, H = P.H;
+    const int x = blockIdx.x * 256 + threadIdx.x;
+    if (x >= W) return;
+    int32_t* cpre = pre + (size_t)(H + 1) * W;
+    const int nc = H / VP_CH + 1;  // chunks holding rows 0 .. H
+    int run = 0;
+    for (int c = 0; c < nc; ++c) {
+        const int t = cpre[(size_t)(c + 1) * W + x];
+        cpre[(size_t)c * W + x] = run;
+        run += t;
+    }
+}
+
+// valid pixels of the inner segment at (yy0, xx0), offsets [-a2, b2] along the inner direction
+__device__ __forceinline__ int seg_votes(const int32_t* __restrict__ pre, bool hf, int H, int W, int yy0, int xx0,
+                                         int a2, int b2) {
+    if (hf) {
+        const int32_t* pr = pre + (size_t)yy0 * (W + 1);
+        return pr[xx0 + b2 + 1] - pr[xx0 - a2];
+    }
+    const int32_t* cpre = pre + (size_t)(H + 1) * W;
+    const int ya = yy0 - a2, yb = yy0 + b2 + 1;
+    return cpre[(size_t)(yb / VP_CH) * W + xx0] + pre[(size_t)yb * W + xx0] -
+           cpre[(size_t)(ya / VP_CH) * W + xx0] - pre[(size_t)ya * W + xx0];
+}
+
 // Vote count of every ranked outlier, 16 lanes an outlier (4 a wave), grid-stride over
 // ranks; lanes take every 16th outer-arm position and a low-vote outlier (every valid
 // sample kept) walks its region again to place its samples at the lanes' prefix slots.
@@ -201,9 +290,9 @@ __global__ __launch_bounds__(256) void k_vote_count_rank(const int32_t* __restri
                                                          const int32_t* __restrict__ out_list,
                                                          const int32_t* __restrict__ counts,
                                                          int32_t* __restrict__ cvote, uint16_t* __restrict__ csamp,
-                                                         uint32_t* __restrict__ vbits, int nb, int hf, DevParams Pk) {
+                                                         const int32_t* __restrict__ vpre, int hf, DevParams Pk) {
     const DevParams P = Pk;
-    pair_shift(blockIdx.z, P.pstride, disp, arms, out_list, counts, cvote, csamp, vbits);
+    pair_shift(blockIdx.z, P.pstride, disp, arms, out_list, counts, cvote, csamp, vpre);
     const int lane = threadIdx.x & 63, sub = lane & 15, base = lane & ~15;
     const int W = P.W, minD = P.minD;
     const int nout = counts[0];
@@ -218,12 +307,26 @@ __global__ __launch_bounds__(256) void k_vote_count_rank(const int32_t* __restri
         const int y = p / W, x = p - y * W;
         int oA = 0, oB = -1, iA, iB;
         if (valid) region_arms(arms[p], hf, oA, oB, iA, iB);
+        // the lane's votes: a prefix difference per inner segment (no pixel walk)
+        auto votes = [&]() {
+            int cnt = 0;
+            for (int o = -oA + sub; o <= oB; o += 16) {
+                const int yy0 = hf ? y + o : y, xx0 = hf ? x : x + o;
+                int a1, b1, a2, b2;
+                region_arms(arms[(size_t)yy0 * W + xx0], hf, a1, b1, a2, b2);
+                cnt += seg_votes(vpre, hf, P.H, W, yy0, xx0, a2, b2);
+            }
+            return cnt;
+        };
+        // a low-vote outlier's samples in the reference's order (segments without a valid
+        // pixel skipped)
         auto walk = [&](bool emit, int pos, uint16_t* smp) {
             int cnt = 0;
             for (int o = -oA + sub; o <= oB; o += 16) {
                 const int yy0 = hf ? y + o : y, xx0 = hf ? x : x + o;
                 int a1, b1, a2, b2;
                 region_arms(arms[(size_t)yy0 * W + xx0], hf, a1, b1, a2, b2);
+                if (seg_votes(vpre, hf, P.H, W, yy0, xx0, a2, b2) == 0) continue;
                 const ptrdiff_t st = hf ? 1 : W;
                 const int32_t* rp = disp + (size_t)yy0 * W + xx0;
                 // the row segment RW_B pixels a round trip (loads issued back to back, then
@@ -242,7 +345,7 @@ __global__ __launch_bounds__(256) void k_vote_count_rank(const int32_t* __restri
             }
             return cnt;
         };
-        const int mine = walk(false, 0, nullptr);
+        const int mine = votes();
         int incl = mine;
 #pragma unroll
         for (int d = 1; d < 16; d <<= 1) {
@@ -251,179 +354,236 @@ __global__ __launch_bounds__(256) void k_vote_count_rank(const int32_t* __restri
         }
         const int total = __shfl(incl, base + 15);
         if (valid && total <= kMaxSamples && mine > 0) walk(true, incl - mine, csamp + (size_t)a * kMaxSamples);
-        if (valid && sub == 0) {
-            cvote[a] = total;
-            if (total > P.voting_thresh) {
-                atomicOr(&vbits[a >> 5], 1u << (a & 31));
-                atomicOr(&vbits[(size_t)nb * VB_L0 + (a >> 10)], 1u << ((a >> 5) & 31));
-            }
-        }
+        if (valid && sub == 0) cvote[a] = total;
     }
 }
 
-// bits 0..b of a word
-__device__ __forceinline__ uint32_t mask_le(int b) { return b >= 31 ? ~0u : (2u << b) - 1u; }
-
-// The nearest high-vote rank below r (-1: none), from the two-level bitmap: the rank's own
-// word, then 64 summary words (65536 ranks) per read.  Wave-uniform.
-__device__ __forceinline__ int prev_high_rank(const uint32_t* __restrict__ l0, const uint32_t* __restrict__ l1,
-                                              int r, int lane) {
-    const int t = r - 1;
-    if (t < 0) return -1;
-    const int u = t >> 5;
-    const uint32_t wd = l0[u] & mask_le(t & 31);
-    if (wd) return u * 32 + 31 - __builtin_clz(wd);
-    for (int v = u - 1; v >= 0; v = ((v >> 5) - 64) * 32 + 31) {
-        const int s = (v >> 5) - lane;
-        uint32_t sw = s >= 0 ? l1[s] : 0u;
-        if (lane == 0) sw &= mask_le(v & 31);
-        const uint64_t ball = __ballot(sw != 0u);
-        if (ball) {
-            const int ln = (int)__builtin_ctzll(ball);
-            const uint32_t swl = (uint32_t)__builtin_amdgcn_readlane((int)sw, ln);
-            const int u2 = ((v >> 5) - ln) * 32 + 31 - __builtin_clz(swl);
-            const uint32_t w2 = l0[u2];
-            return u2 * 32 + 31 - __builtin_clz(w2);
-        }
-        if ((v >> 5) < 64) break;
+// The high-vote outliers (vote > votingThresh, :1132) listed in rank order: hv_list[k] = the
+// rank of the k-th one, counts[1] = how many.  Two launches over the ranks, as the outlier
+// ranking (per-block counts in bsum[2 b + 1], then the scatter).
+__device__ __forceinline__ int hv_flags(const int32_t* __restrict__ cvote, int base, int nout, int thresh,
+                                        int (&f)[SC_ITEMS]) {
+    int c = 0;
+#pragma unroll
+    for (int k = 0; k < SC_ITEMS; ++k) {
+        f[k] = base + k < nout && cvote[base + k] > thresh ? 1 : 0;
+        c += f[k];
     }
-    return -1;
+    return c;
 }
 
-// The high-vote ranked outliers by quarter words of the bitmap (up to 8 ranks, grid-stride):
-// wave j of the workgroup builds rank r_j's LDS histogram of its own region, the whole
-// workgroup then adds the samples of the low-vote outliers ranked between the previous
-// high-vote one (found in the bitmap) and each r_j -- the histogram the reference carries in
-// raster order (:1132-1151) -- VD_CB ranks a thread per round trip, and wave j takes the first
-// argmax and the ratio test (:1137-1153).
-constexpr int VD_CB = 8;
-__global__ __launch_bounds__(VD_THREADS) void k_vote_decide_rank(
+__global__ void k_hv_count(const int32_t* __restrict__ cvote, const int32_t* __restrict__ counts,
+                           int32_t* __restrict__ bsum, int thresh, size_t ps) {
+    pair_shift(blockIdx.z, ps, cvote, counts, bsum);
+    __shared__ int sa[SC_THREADS], sb[SC_THREADS];
+    const int nout = counts[0];
+    const int base = blockIdx.x * SC_BLOCK + threadIdx.x * SC_ITEMS;
+    int f[SC_ITEMS];
+    int a = base < nout ? hv_flags(cvote, base, nout, thresh, f) : 0, b = 0;
+    block_scan2(a, b, sa, sb);
+    if (threadIdx.x == SC_THREADS - 1) bsum[2 * blockIdx.x + 1] = sa[SC_THREADS - 1];
+}
+
+__global__ void k_hv_scatter(const int32_t* __restrict__ cvote, int32_t* __restrict__ counts,
+                             const int32_t* __restrict__ bsum, int32_t* __restrict__ hv_list, int thresh, size_t ps) {
+    pair_shift(blockIdx.z, ps, cvote, counts, bsum, hv_list);
+    __shared__ int s_base;
+    if (threadIdx.x == 0) s_base = 0;
+    __syncthreads();
+    {
+        int part = 0;
+        for (int i = threadIdx.x; i < (int)blockIdx.x; i += SC_THREADS) part += bsum[2 * i + 1];
+        if (part) atomicAdd(&s_base, part);
+    }
+    __shared__ int sa[SC_THREADS], sb[SC_THREADS];
+    const int nout = counts[0];
+    const int base = blockIdx.x * SC_BLOCK + threadIdx.x * SC_ITEMS;
+    int f[SC_ITEMS];
+    int a = 0, b = 0;
+    if (base < nout) a = hv_flags(cvote, base, nout, thresh, f);
+    else {
+#pragma unroll
+        for (int k = 0; k < SC_ITEMS; ++k) f[k] = 0;
+    }
+    block_scan2(a, b, sa, sb);  // its barriers also publish s_base
+    a += s_base;
+    if (threadIdx.x == SC_THREADS - 1 && blockIdx.x == gridDim.x - 1) counts[1] = s_base + sa[SC_THREADS - 1];
+#pragma unroll
+    for (int k = 0; k < SC_ITEMS; ++k)
+        if (f[k]) hv_list[a++] = base + k;
+}
+
+// The decision, one wave per high-vote outlier r_k (grid-stride over k): its own region into a
+// wave-private LDS histogram, then the samples of the low-vote outliers ranked between the
+// previous high-vote one r_{k-1} and r_k -- exactly the histogram the reference carries in
+// raster order (:1132-1151: hist is cleared only by a high-vote decision) -- then the first
+// argmax and the ratio test (:1137-1153).  No workgroup barrier: every wave is independent.
+constexpr int VD_WAVES = 4;
+constexpr int VD_CB = 8;      // carried votes loaded a lane per round trip (512 ranks a wave)
+constexpr int VD_LONG = 2048; // carries longer than this go to k_vote_decide_long (a workgroup a rank)
+__global__ __launch_bounds__(VD_WAVES * 64) void k_vote_decide_wave(
     const int32_t* __restrict__ disp, int32_t* __restrict__ dtmp, const uint32_t* __restrict__ arms,
     const int32_t* __restrict__ out_list, const int32_t* __restrict__ cvote, const uint16_t* __restrict__ csamp,
-    const int32_t* __restrict__ counts, const uint32_t* __restrict__ vbits, int nb, int hf, DevParams Pk) {
+    int32_t* __restrict__ counts, const int32_t* __restrict__ hv_list, int32_t* __restrict__ long_list, int hf,
+    DevParams Pk) {
     const DevParams P = Pk;
-    pair_shift(blockIdx.z, P.pstride, disp, dtmp, arms, out_list, cvote, csamp, counts, vbits);
+    pair_shift(blockIdx.z, P.pstride, disp, dtmp, arms, out_list, cvote, csamp, counts, hv_list, long_list);
+    extern __shared__ int hist[];
+    const int L = P.L, W = P.W, minD = P.minD;
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    int* h = hist + wv * L;
+    const int nhv = counts[1];
+    for (int k = blockIdx.x * VD_WAVES + wv; k < nhv; k += gridDim.x * VD_WAVES) {
+        const int r = hv_list[k];
+        const int prev = k > 0 ? hv_list[k - 1] : -1;
+        if (r - prev - 1 > VD_LONG) {  // a long carry: a whole workgroup takes it (next launch)
+            if (lane == 0) long_list[atomicAdd(&counts[2], 1)] = k;
+            continue;
+        }
+        for (int d = lane; d < L; d += 64) h[d] = 0;  // a wave's LDS operations stay in order
+        const int p = out_list[r];
+        const int v = cvote[r];
+        const int y = p / W, x = p - y * W;
+        int oA, oB, iA, iB;
+        region_arms(arms[p], hf, oA, oB, iA, iB);
+        // a region is mostly one or two disparities: each lane counts into a private two-entry
+        // cache and adds an entry to the histogram only when it is evicted (64 lanes' atomics on
+        // one bin serialise); the counts are exact either way
+        int cd0 = -1, cn0 = 0, cd1 = -1, cn1 = 0;
+        for (int o = -oA + lane; o <= oB; o += 64) {
+            const int yy0 = hf ? y + o : y, xx0 = hf ? x : x + o;
+            int a1, b1, a2, b2;
+            region_arms(arms[(size_t)yy0 * W + xx0], hf, a1, b1, a2, b2);
+            const ptrdiff_t st = hf ? 1 : W;
+            const int32_t* rp = disp + (size_t)yy0 * W + xx0;
+            for (int i = -a2; i <= b2; i += RW_B) {  // RW_B loads a round trip
+                int dv[RW_B];
+#pragma unroll
+                for (int kk = 0; kk < RW_B; ++kk) dv[kk] = i + kk <= b2 ? rp[(ptrdiff_t)(i + kk) * st] : -1;
+#pragma unroll
+                for (int kk = 0; kk < RW_B; ++kk) {
+                    const int d = dv[kk];
+                    if (d >= minD) {
+                        if (d == cd0) ++cn0;
+                        else if (d == cd1) ++cn1;
+                        else {
+                            if (cn1) atomicAdd(&h[cd1 - minD], cn1);
+                            cd1 = cd0; cn1 = cn0; cd0 = d; cn0 = 1;
+                        }
+                    }
+                }
+            }
+        }
+        if (cn0) atomicAdd(&h[cd0 - minD], cn0);
+        if (cn1) atomicAdd(&h[cd1 - minD], cn1);
+        // the carried samples: low-vote outliers ranked in (prev, r), VD_CB * 64 votes a round
+        // trip (synthetic scenes carry thousands of ranks, most without a sample)
+        for (int kb = prev + 1; kb < r; kb += VD_CB * 64) {
+            int c[VD_CB];
+#pragma unroll
+            for (int j = 0; j < VD_CB; ++j) {
+                const int kk = kb + j * 64 + lane;
+                c[j] = kk < r ? cvote[kk] : 0;
+            }
+#pragma unroll
+            for (int j = 0; j < VD_CB; ++j) {
+                if (c[j] > 0 && c[j] <= P.voting_thresh) {
+                    const int kk = kb + j * 64 + lane;
+                    const uint32_t* sp = reinterpret_cast<const uint32_t*>(csamp + (size_t)kk * kMaxSamples);
+                    uint32_t w2[kMaxSamples / 2];
+#pragma unroll
+                    for (int i = 0; i < kMaxSamples / 2; ++i) w2[i] = sp[i];
+#pragma unroll
+                    for (int m = 0; m < kMaxSamples; ++m)
+                        if (m < c[j]) atomicAdd(&h[(w2[m >> 1] >> (16 * (m & 1))) & 0xffffu], 1);
+                }
+            }
+        }
+        uint64_t best = ~0ull;
+        for (int d = lane; d < L; d += 64) {
+            const uint64_t key = ((uint64_t)(0xffffffffu - (uint32_t)h[d]) << 32) | (uint32_t)d;
+            best = key < best ? key : best;
+        }
+        best = wave_min_u64(best);
+        const int cmax = (int)(0xffffffffu - (uint32_t)(best >> 32));
+        const int dbest = (int)(uint32_t)best;
+        const float ratio = cmax / (float)v;
+        if (lane == 0) dtmp[p] = ratio > P.voting_ratio && cmax > 0 ? dbest + minD : disp[p];
+    }
+}
+
+// The high-vote outliers whose carry is longer than VD_LONG ranks (synthetic scenes: a few
+// per pass, carrying thousands of low-vote outliers), a workgroup each: the region split over
+// its threads by outer position, the carry over all its threads, then the same decision.
+constexpr int VL_THREADS = 512;
+__global__ __launch_bounds__(VL_THREADS) void k_vote_decide_long(
+    const int32_t* __restrict__ disp, int32_t* __restrict__ dtmp, const uint32_t* __restrict__ arms,
+    const int32_t* __restrict__ out_list, const int32_t* __restrict__ cvote, const uint16_t* __restrict__ csamp,
+    const int32_t* __restrict__ counts, const int32_t* __restrict__ hv_list, const int32_t* __restrict__ long_list,
+    int hf, DevParams Pk) {
+    const DevParams P = Pk;
+    pair_shift(blockIdx.z, P.pstride, disp, dtmp, arms, out_list, cvote, csamp, counts, hv_list, long_list);
     extern __shared__ int hist[];
     const int L = P.L, W = P.W, minD = P.minD;
     const int tid = threadIdx.x, lane = tid & 63;
-    const uint32_t* l0 = vbits;
-    const uint32_t* l1 = vbits + (size_t)nb * VB_L0;
-    const int nout = counts[0];
-    const int nwords = (nout + 31) >> 5;
-    // workgroup b takes bits [8q, 8q + 8) (q = b mod 4) of the words b / 4 + k G4: clustered
-    // high-vote outliers (tens to a word) are spread over four workgroups.  Its words are
-    // read in one round trip (a thread each) and the non-empty ones listed in LDS.
-    __shared__ uint32_t s_list[VD_THREADS][2];  // kVdStaticLds bytes
-    __shared__ int s_n;
-    const int q = blockIdx.x & 3, G4 = gridDim.x >> 2, w0 = blockIdx.x >> 2;
-    const int nk = w0 < nwords ? (nwords - w0 + G4 - 1) / G4 : 0;
-    for (int kb = 0; kb < nk; kb += VD_THREADS) {
-        if (tid == 0) s_n = 0;
+    const int nlong = counts[2];
+    for (int i = blockIdx.x; i < nlong; i += gridDim.x) {
+        const int k = long_list[i];
+        const int r = hv_list[k];
+        const int prev = k > 0 ? hv_list[k - 1] : -1;
+        for (int d = tid; d < L; d += VL_THREADS) hist[d] = 0;
         __syncthreads();
-        if (kb + tid < nk) {
-            const int wi = w0 + (kb + tid) * G4;
-            const uint32_t wd = l0[wi] & (0xffu << (8 * q));
-            if (wd) {
-                const int slot = atomicAdd(&s_n, 1);
-                s_list[slot][0] = (uint32_t)wi;
-                s_list[slot][1] = wd;
+        const int p = out_list[r];
+        const int v = cvote[r];
+        const int y = p / W, x = p - y * W;
+        int oA, oB, iA, iB;
+        region_arms(arms[p], hf, oA, oB, iA, iB);
+        for (int o = -oA + tid; o <= oB; o += VL_THREADS) {
+            const int yy0 = hf ? y + o : y, xx0 = hf ? x : x + o;
+            int a1, b1, a2, b2;
+            region_arms(arms[(size_t)yy0 * W + xx0], hf, a1, b1, a2, b2);
+            const ptrdiff_t st = hf ? 1 : W;
+            const int32_t* rp = disp + (size_t)yy0 * W + xx0;
+            for (int ii = -a2; ii <= b2; ++ii) {
+                const int d = rp[(ptrdiff_t)ii * st];
+                if (d >= minD) atomicAdd(&hist[d - minD], 1);
+            }
+        }
+        for (int kb = prev + 1; kb < r; kb += VD_CB * VL_THREADS) {
+            int c[VD_CB];
+#pragma unroll
+            for (int j = 0; j < VD_CB; ++j) {
+                const int kk = kb + j * VL_THREADS + tid;
+                c[j] = kk < r ? cvote[kk] : 0;
+            }
+#pragma unroll
+            for (int j = 0; j < VD_CB; ++j) {
+                if (c[j] > 0 && c[j] <= P.voting_thresh) {
+                    const int kk = kb + j * VL_THREADS + tid;
+                    const uint32_t* sp = reinterpret_cast<const uint32_t*>(csamp + (size_t)kk * kMaxSamples);
+                    uint32_t w2[kMaxSamples / 2];
+#pragma unroll
+                    for (int ii = 0; ii < kMaxSamples / 2; ++ii) w2[ii] = sp[ii];
+#pragma unroll
+                    for (int m = 0; m < kMaxSamples; ++m)
+                        if (m < c[j]) atomicAdd(&hist[(w2[m >> 1] >> (16 * (m & 1))) & 0xffffu], 1);
+                }
             }
         }
         __syncthreads();
-        const int nl = s_n;
-        for (int li = 0; li < nl; ++li) {
-            // the quarter word's high-vote ranks r_0 < ... < r_{nr-1}: no other high-vote rank
-            // lies between them, so r_j's carry is (r_{j-1}, r_j) and r_0's is (prev, r_0)
-            const int wi = (int)s_list[li][0];
-            const uint32_t word = s_list[li][1];
-            const int nr = __builtin_popcount(word);
-            for (int d = tid; d < nr * L; d += VD_THREADS) hist[d] = 0;
-            int rk[8];
-            {
-                uint32_t wb = word;
-#pragma unroll
-                for (int j = 0; j < 8; ++j) {
-                    rk[j] = wb ? wi * 32 + (int)__builtin_ctz(wb) : 0x7fffffff;
-                    wb &= wb - 1u;
-                }
+        if (tid < 64) {
+            uint64_t best = ~0ull;
+            for (int d = lane; d < L; d += 64) {
+                const uint64_t key = ((uint64_t)(0xffffffffu - (uint32_t)hist[d]) << 32) | (uint32_t)d;
+                best = key < best ? key : best;
             }
-            __syncthreads();
-            // wave j: the own region of r_j into histogram j
-            const int wv = tid >> 6;
-            int p = 0, v = 0;
-            if (wv < nr) {
-                int r = rk[0];
-#pragma unroll
-                for (int j = 1; j < 8; ++j) r = wv == j ? rk[j] : r;
-                v = cvote[r];
-                p = out_list[r];
-                const int y = p / W, x = p - y * W;
-                int oA, oB, iA, iB;
-                region_arms(arms[p], hf, oA, oB, iA, iB);
-                int* h = hist + wv * L;
-                for (int o = -oA + lane; o <= oB; o += 64) {
-                    const int yy0 = hf ? y + o : y, xx0 = hf ? x : x + o;
-                    int a1, b1, a2, b2;
-                    region_arms(arms[(size_t)yy0 * W + xx0], hf, a1, b1, a2, b2);
-                    const ptrdiff_t st = hf ? 1 : W;
-                    const int32_t* rp = disp + (size_t)yy0 * W + xx0;
-                    for (int i = -a2; i <= b2; i += RW_B) {  // RW_B loads a round trip
-                        int dv[RW_B];
-#pragma unroll
-                        for (int k = 0; k < RW_B; ++k) dv[k] = i + k <= b2 ? rp[(ptrdiff_t)(i + k) * st] : -1;
-#pragma unroll
-                        for (int k = 0; k < RW_B; ++k)
-                            if (dv[k] >= minD) atomicAdd(&h[dv[k] - minD], 1);
-                    }
-                }
-            }
-            // carried: the low-vote ranks with samples in (prev, r_last), each into the
-            // histogram of the first r_j above it, VD_CB ranks a thread per round trip
-            const int lo = prev_high_rank(l0, l1, rk[0], lane) + 1;
-            int rlast = rk[0];
-#pragma unroll
-            for (int j = 1; j < 8; ++j) rlast = j < nr ? rk[j] : rlast;
-            for (int base = lo; base < rlast; base += VD_CB * VD_THREADS) {
-                int ck[VD_CB];
-#pragma unroll
-                for (int c = 0; c < VD_CB; ++c) {
-                    const int k = base + c * VD_THREADS + tid;
-                    ck[c] = k < rlast ? cvote[k] : 0;
-                }
-#pragma unroll
-                for (int c = 0; c < VD_CB; ++c) {
-                    if (ck[c] > 0 && ck[c] <= P.voting_thresh) {
-                        const int k = base + c * VD_THREADS + tid;
-                        int j = 0;
-#pragma unroll
-                        for (int t = 0; t < 7; ++t) j += k > rk[t] ? 1 : 0;
-                        int* h = hist + j * L;
-                        const uint32_t* s = reinterpret_cast<const uint32_t*>(csamp + (size_t)k * kMaxSamples);
-                        uint32_t wv2[kMaxSamples / 2];
-#pragma unroll
-                        for (int i = 0; i < kMaxSamples / 2; ++i) wv2[i] = s[i];
-#pragma unroll
-                        for (int m = 0; m < kMaxSamples; ++m)
-                            if (m < ck[c]) atomicAdd(&h[(wv2[m >> 1] >> (16 * (m & 1))) & 0xffffu], 1);
-                    }
-                }
-            }
-            __syncthreads();
-            if (wv < nr) {  // wave j: first argmax of histogram j, the ratio test
-                const int* h = hist + wv * L;
-                uint64_t best = ~0ull;
-                for (int d = lane; d < L; d += 64) {
-                    const uint64_t key = ((uint64_t)(0xffffffffu - (uint32_t)h[d]) << 32) | (uint32_t)d;
-                    best = key < best ? key : best;
-                }
-                best = wave_min_u64(best);
-                const int cmax = (int)(0xffffffffu - (uint32_t)(best >> 32));
-                const int dbest = (int)(uint32_t)best;
-                const float ratio = cmax / (float)v;
-                if (lane == 0) dtmp[p] = ratio > P.voting_ratio && cmax > 0 ? dbest + minD : disp[p];
-            }
-            __syncthreads();
+            best = wave_min_u64(best);
+            const int cmax = (int)(0xffffffffu - (uint32_t)(best >> 32));
+            const int dbest = (int)(uint32_t)best;
+            const float ratio = cmax / (float)v;
+            if (lane == 0) dtmp[p] = ratio > P.voting_ratio && cmax > 0 ? dbest + minD : disp[p];
         }
+        __syncthreads();
     }
 }
 
@@ -904,7 +1064,7 @@ __global__ void k_arms_to_ref(const uint32_t* __restrict__ arms, int32_t* __rest
 // launchers
 // ---------------------------------------------------------------------------
 size_t refine_scan_blocks(int n) { return (size_t)(n + SC_BLOCK - 1) / SC_BLOCK; }
-size_t refine_vote_bits_bytes(int n) { return vote_bits_words((int)refine_scan_blocks(n)) * 4; }
+
 
 // every refinement launch covers the group's P.npairs pairs (blockIdx.z = pair)
 static dim3 grid2d(int W, int H, int bx, const DevParams& P) { return dim3((W + bx - 1) / bx, H, P.npairs); }
@@ -924,24 +1084,38 @@ void launch_region_voting(RefineBufs& B, const uint32_t* arms0, int hf, const De
     hipLaunchKernelGGL(k_oscan_count, grid1d(nb, P), dim3(SC_THREADS), 0, st, B.dm, n, P.minD, B.bsum, ps);
     trace_point("k_oscan_count", st);
     hipLaunchKernelGGL(k_oscan_scatter, grid1d(nb, P), dim3(SC_THREADS), 0, st, B.dm, n, P.minD, B.bsum,
-                       B.out_list, B.dtmp, B.vbits, B.counts, ps);
+                       B.out_list, B.dtmp, B.counts, ps);
     trace_point("k_oscan_scatter", st);
+    if (hf) {
+        hipLaunchKernelGGL(k_vprefix_rows, grid1d(P.H, P), dim3(256), 0, st, B.dm, B.vpre, P);
+        trace_point("k_vprefix_rows", st);
+    } else {
+        hipLaunchKernelGGL(k_vprefix_cols, dim3((P.W + 255) / 256, P.H / VP_CH + 1, P.npairs), dim3(256), 0, st,
+                           B.dm, B.vpre, P);
+        hipLaunchKernelGGL(k_vprefix_cols_scan, dim3((P.W + 255) / 256, 1, P.npairs), dim3(256), 0, st, B.vpre, P);
+        trace_point("k_vprefix_cols", st);
+    }
     // grid-stride over the ranked outliers (their count stays on the device)
     // latency-bound walks: single pairs take enough waves to keep every SIMD several deep
     const int vc_blocks = std::max(64, 4096 / std::max(1, P.npairs));
     hipLaunchKernelGGL(k_vote_count_rank, grid1d(vc_blocks, P), dim3(256), 0, st, B.dm, arms0, B.out_list,
-                       B.counts, B.cvote, B.csamp, B.vbits, nb, hf, P);
+                       B.counts, B.cvote, B.csamp, B.vpre, hf, P);
     trace_point("k_vote_count_rank", st);
-    // grid-stride over quarter words of the bitmap, one round of resident workgroups (a
-    // workgroup per quarter word of a full image's ranks measured 32 us a launch, most idle)
-    const size_t lds = (size_t)8 * P.L * sizeof(int);  // a histogram per rank of a quarter word
-    // the attribute covers dynamic LDS only; with the static rank list it must fit the CU
-    static_assert(8 * 2048 * sizeof(int) + kVdStaticLds <= 160 * 1024, "vote-decision LDS past 160 KB");
-    const int vd_blocks = 4 * std::max(16, 256 / std::max(1, P.npairs));
-    ensure_lds_limit((const void*)k_vote_decide_rank, lds);
-    hipLaunchKernelGGL(k_vote_decide_rank, grid1d(vd_blocks, P), dim3(VD_THREADS), lds, st, B.dm, B.dtmp,
-                       arms0, B.out_list, B.cvote, B.csamp, B.counts, B.vbits, nb, hf, P);
-    trace_point("k_vote_decide_rank", st);
+    hipLaunchKernelGGL(k_hv_count, grid1d(nb, P), dim3(SC_THREADS), 0, st, B.cvote, B.counts, B.bsum,
+                       P.voting_thresh, ps);
+    hipLaunchKernelGGL(k_hv_scatter, grid1d(nb, P), dim3(SC_THREADS), 0, st, B.cvote, B.counts, B.bsum, B.hv_list,
+                       P.voting_thresh, ps);
+    trace_point("k_hv_scatter", st);
+    // one wave per high-vote outlier, grid-stride; a histogram of L ints per wave
+    const size_t lds = (size_t)VD_WAVES * P.L * sizeof(int);
+    static_assert((size_t)VD_WAVES * 2048 * sizeof(int) <= 64 * 1024, "vote-decision LDS past the default limit");
+    const int vd_blocks = std::max(64, 4096 / std::max(1, P.npairs));
+    hipLaunchKernelGGL(k_vote_decide_wave, grid1d(vd_blocks, P), dim3(VD_WAVES * 64), lds, st, B.dm, B.dtmp, arms0,
+                       B.out_list, B.cvote, B.csamp, B.counts, B.hv_list, B.long_list, hf, P);
+    trace_point("k_vote_decide_wave", st);
+    hipLaunchKernelGGL(k_vote_decide_long, grid1d(64, P), dim3(VL_THREADS), (size_t)P.L * sizeof(int), st, B.dm,
+                       B.dtmp, arms0, B.out_list, B.cvote, B.csamp, B.counts, B.hv_list, B.long_list, hf, P);
+    trace_point("k_vote_decide_long", st);
     std::swap(B.dm, B.dtmp);
 }
 

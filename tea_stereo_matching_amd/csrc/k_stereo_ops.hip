@@ -429,6 +429,151 @@ __global__ void k_remap_fixed(Tab<const uint8_t> srcs, int sh, int sw, size_t ss
     store_px<C>(dst + (size_t)p.y * dstep + (size_t)p.x0 * C, n, o);
 }
 
+// Tiled form of k_remap_fixed: rectification maps are near-identity warps, so a tile of
+// RT_ROWS x RT_COLS outputs reads a small source window.  The workgroup reduces its maps'
+// bounding box, stages the box (clamped to the image) in LDS with coalesced dword loads,
+// and every tap is then an LDS read instead of a per-pixel gather through the texture
+// path (two rows x three dwords a pixel).  A box past RT_LDS_DW dwords (arbitrary maps)
+// takes the direct per-pixel path for the whole tile.  Same arithmetic as remap_px.
+constexpr int RT_TX = 32;                      // lanes along a tile row (4 pixels each)
+constexpr int RT_ROWS = OPS_THREADS / RT_TX;   // 8
+constexpr int RT_COLS = RT_TX * OPS_PX;        // 128
+constexpr int RT_LDS_DW = 6144;                // 24 KB of staged source a workgroup
+
+template <int C>
+__device__ __forceinline__ void lds_taps(const uint32_t* __restrict__ box, int pitch_dw, int by0, int cb0,
+                                         int sh, int sw, int sx, int sy, uint32_t (&b)[2 * C]) {
+    if (sy < 0 || sy >= sh) {
+#pragma unroll
+        for (int i = 0; i < 2 * C; ++i) b[i] = 0;
+        return;
+    }
+    const uint32_t* row = box + (sy - by0) * pitch_dw;
+    if (sx >= 0 && sx + 1 < sw) {  // both taps in the image: 2C bytes from <= 3 dwords
+        const int o = sx * C - cb0;
+        const uint32_t* w = row + (o >> 2);
+        const uint32_t w0 = w[0], w1 = w[1], w2 = (2 * C + (o & 3) > 8) ? w[2] : 0u;
+        const uint32_t s8 = (uint32_t)(o & 3) * 8;
+        const uint32_t lo = __builtin_amdgcn_alignbit(w1, w0, s8);
+        const uint32_t hi = __builtin_amdgcn_alignbit(w2, w1, s8);
+#pragma unroll
+        for (int i = 0; i < 2 * C; ++i) b[i] = ((i < 4 ? lo : hi) >> (8 * (i & 3))) & 0xffu;
+        return;
+    }
+#pragma unroll
+    for (int t = 0; t < 2; ++t) {
+        const int x = sx + t;
+        const bool in = x >= 0 && x < sw;
+#pragma unroll
+        for (int c = 0; c < C; ++c) {
+            const int o = x * C + c - cb0;
+            b[t * C + c] = in ? (row[o >> 2] >> (8 * (o & 3))) & 0xffu : 0u;
+        }
+    }
+}
+
+__device__ __forceinline__ int block_reduce(int v, bool mx, int* red, int slot) {
+#pragma unroll
+    for (int s = 32; s >= 1; s >>= 1) {
+        const int o = __shfl_xor(v, s);
+        v = mx ? max(v, o) : min(v, o);
+    }
+    const int wv = threadIdx.x >> 6;
+    if ((threadIdx.x & 63) == 0) red[slot * 4 + wv] = v;
+    __syncthreads();
+    int r = red[slot * 4];
+#pragma unroll
+    for (int k = 1; k < OPS_THREADS / 64; ++k) r = mx ? max(r, red[slot * 4 + k]) : min(r, red[slot * 4 + k]);
+    return r;
+}
+
+// src must be 4-B aligned with a row step that is a multiple of 4 (the launcher checks):
+// then every source row starts on a dword and the staged rows need no per-row shift.
+template <int C>
+__global__ __launch_bounds__(OPS_THREADS) void k_remap_tile(Tab<const uint8_t> srcs, int sh, int sw, size_t sstep,
+                                                            const int16_t* __restrict__ xy, size_t xy_step_e,
+                                                            const uint16_t* __restrict__ fxy, size_t fxy_step_e,
+                                                            int rows, int cols, Tab<uint8_t> dsts, size_t dstep) {
+    __shared__ uint32_t box[RT_LDS_DW];
+    __shared__ int red[4 * (OPS_THREADS / 64)];
+    const uint8_t* __restrict__ src = srcs.p[blockIdx.z];
+    uint8_t* __restrict__ dst = dsts.p[blockIdx.z];
+    const int y = blockIdx.y * RT_ROWS + (int)threadIdx.x / RT_TX;
+    const int x0 = blockIdx.x * RT_COLS + ((int)threadIdx.x % RT_TX) * OPS_PX;
+    const int n = (y < rows && x0 < cols) ? min(OPS_PX, cols - x0) : 0;
+    uint32_t mxy[OPS_PX], mf[OPS_PX];
+    if (n > 0) {
+        const int16_t* xr = xy + (size_t)y * xy_step_e + 2 * (size_t)x0;
+        const uint16_t* fr = fxy + (size_t)y * fxy_step_e + x0;
+        if (n == OPS_PX && ((uintptr_t)xr & 15) == 0 && ((uintptr_t)fr & 7) == 0) {
+            const uint4 a = *reinterpret_cast<const uint4*>(xr);
+            const uint2 b = *reinterpret_cast<const uint2*>(fr);
+            mxy[0] = a.x; mxy[1] = a.y; mxy[2] = a.z; mxy[3] = a.w;
+            mf[0] = b.x; mf[1] = b.x >> 16; mf[2] = b.y; mf[3] = b.y >> 16;
+        } else {
+#pragma unroll
+            for (int k = 0; k < OPS_PX; ++k) {
+                const int kk = k < n ? k : n - 1;
+                mxy[k] = (uint32_t)(uint16_t)xr[2 * kk] | ((uint32_t)(uint16_t)xr[2 * kk + 1] << 16);
+                mf[k] = fr[kk];
+            }
+        }
+    }
+    // bounding box of the tile's taps (x .. x+1, y .. y+1), clamped to the image
+    int lx = 0x7fffffff, hx = -0x7fffffff, ly = 0x7fffffff, hy = -0x7fffffff;
+#pragma unroll
+    for (int k = 0; k < OPS_PX; ++k) {
+        if (k < n) {
+            const int sx = (int)(int16_t)(mxy[k] & 0xffffu), sy = (int)(int16_t)(mxy[k] >> 16);
+            lx = min(lx, sx); hx = max(hx, sx + 1);
+            ly = min(ly, sy); hy = max(hy, sy + 1);
+        }
+    }
+    const int bx0 = max(block_reduce(lx, false, red, 0), 0), bx1 = min(block_reduce(hx, true, red, 1), sw - 1);
+    const int by0 = max(block_reduce(ly, false, red, 2), 0), by1 = min(block_reduce(hy, true, red, 3), sh - 1);
+    const int cb0 = (bx0 * C) & ~3;                              // first staged byte of a row
+    const int pitch_dw = ((bx1 + 1) * C - cb0 + 3) / 4 + 1;     // + 1: the 3-dword tap reads
+    const int nbr = by1 - by0 + 1;
+    const bool staged = bx0 <= bx1 && by0 <= by1 && (long)nbr * pitch_dw <= RT_LDS_DW;
+    if (staged) {
+        const size_t end = (size_t)(sh - 1) * sstep + (size_t)sw * C;  // bytes of the image
+        for (int i = threadIdx.x; i < nbr * pitch_dw; i += OPS_THREADS) {
+            const int r = i / pitch_dw, c = i - r * pitch_dw;
+            const size_t off = (size_t)(by0 + r) * sstep + (size_t)cb0 + 4 * (size_t)c;
+            uint32_t v = 0;
+            if (off + 4 <= end) {
+                v = *reinterpret_cast<const uint32_t*>(src + off);
+            } else {
+                for (int k = 0; k < 4; ++k) v |= off + k < end ? (uint32_t)src[off + k] << (8 * k) : 0u;
+            }
+            box[i] = v;
+        }
+        __syncthreads();
+    }
+    if (n == 0) return;
+    uint32_t o[OPS_PX][C];
+#pragma unroll
+    for (int k = 0; k < OPS_PX; ++k) {
+        const int sx = (int)(int16_t)(mxy[k] & 0xffffu);
+        const int sy = (int)(int16_t)(mxy[k] >> 16);
+        const int f = (int)(mf[k] & 1023u);
+        if (staged) {
+            const int fx = f & 31, fy = f >> 5;
+            const uint32_t w00 = (uint32_t)((32 - fx) * (32 - fy) * 32), w01 = (uint32_t)(fx * (32 - fy) * 32);
+            const uint32_t w10 = (uint32_t)((32 - fx) * fy * 32), w11 = (uint32_t)(fx * fy * 32);
+            uint32_t t0[2 * C], t1[2 * C];
+            lds_taps<C>(box, pitch_dw, by0, cb0, sh, sw, sx, sy, t0);
+            lds_taps<C>(box, pitch_dw, by0, cb0, sh, sw, sx, sy + 1, t1);
+#pragma unroll
+            for (int c = 0; c < C; ++c)
+                o[k][c] = (t0[c] * w00 + t0[C + c] * w01 + t1[c] * w10 + t1[C + c] * w11 + (1u << 14)) >> 15;
+        } else {
+            remap_px<C>(src, sh, sw, sstep, sx, sy, f & 31, f >> 5, o[k]);
+        }
+    }
+    store_px<C>(dst + (size_t)y * dstep + (size_t)x0 * C, n, o);
+}
+
 // saturate_cast<int>(v * 32) = cvRound, x86: nearest-even, NaN / out of range -> INT_MIN
 __device__ __forceinline__ int round32(float v) {
     const float a = v * 32.f;
@@ -789,6 +934,25 @@ int tsm_remap_linear_fixed_batch_device(int n, const uint8_t* const* d_srcs, int
         xy_step < 4 * (size_t)cols || fxy_step < 2 * (size_t)cols || dst_step < (size_t)C * cols)
         return TSM_ERR_ARGUMENT;
     hipStream_t st = (hipStream_t)hip_stream;
+    // the LDS-tiled form when every source row starts on a dword (the usual case)
+    bool aligned = src_step % 4 == 0;
+    for (int i = 0; i < n && aligned; ++i) aligned = ((uintptr_t)d_srcs[i] & 3) == 0;
+    if (aligned) {
+        for (int i = 0; i < n; i += kOpsBatch) {
+            const int k = min(kOpsBatch, n - i);
+            const dim3 g((cols + RT_COLS - 1) / RT_COLS, (rows + RT_ROWS - 1) / RT_ROWS, k);
+            const Tab<const uint8_t> s = tab_of<const uint8_t>(d_srcs + i, k);
+            const Tab<uint8_t> d = tab_of<uint8_t>(d_dsts + i, k);
+#define TSM_REMAP_TILE(CC)                                                                               \
+            hipLaunchKernelGGL(k_remap_tile<CC>, g, dim3(OPS_THREADS), 0, st, s, src_rows, src_cols, src_step, \
+                               d_xy, xy_step / 2, d_fxy, fxy_step / 2, rows, cols, d, dst_step)
+            if (C == 1) TSM_REMAP_TILE(1);
+            else if (C == 3) TSM_REMAP_TILE(3);
+            else TSM_REMAP_TILE(4);
+#undef TSM_REMAP_TILE
+        }
+        return status(hipGetLastError());
+    }
     // packed maps and output run as one row (the source is addressed through the maps)
     const bool dense = xy_step == 4 * (size_t)cols && fxy_step == 2 * (size_t)cols && dst_step == (size_t)C * cols &&
                        (long)rows * cols <= 0x7fffffffL;

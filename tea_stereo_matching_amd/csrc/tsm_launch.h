@@ -68,7 +68,8 @@ struct RefineBufs {
     int32_t* cvote;   // [H][W] vote count by outlier rank (out_pos order)
     uint16_t* csamp;  // [H][W][20] low-vote samples by outlier rank
     int32_t* bsum;    // scan block sums [2 * nblocks]
-    uint32_t* vbits;  // high-vote rank bitmaps: nblocks * (128 level-0 + 4 level-1 words)
+    int32_t* hv_list; // [H][W] ranks of the high-vote outliers of a voting pass, in rank order
+    int32_t* long_list; // [H][W] indices into hv_list of the ranks with long carries
     int32_t* counts;  // [4]
     uint8_t* gray;    // [H][W]
     int32_t* hist;    // [256] + 64 ints of LUT scratch
@@ -82,9 +83,11 @@ struct RefineBufs {
     uint8_t* strong;  // [H][W]
     uint8_t* edges;   // [H][W]
     float* subpix;    // [H][W]
+    int32_t* vpre;    // valid-pixel prefix counts of a voting pass (refine_vpre_ints)
 };
+// ints of RefineBufs.vpre: rows (H x (W+1)) or columns ((H+1) x W + chunk prefixes)
+size_t refine_vpre_ints(int H, int W);
 size_t refine_scan_blocks(int n);
-size_t refine_vote_bits_bytes(int n);
 void launch_outlier(RefineBufs& B, const DevParams& P, hipStream_t st);
 void launch_region_voting(RefineBufs& B, const uint32_t* arms0, int horizontal_first,
                           const DevParams& P, hipStream_t st);

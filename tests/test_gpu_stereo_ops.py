@@ -180,6 +180,30 @@ def test_remap_bit_exact(tsm, oracle, C, H, W):
     assert np.array_equal(tsm.remap(src, mx, my), oracle.remap_linear_float(src, mx, my))
 
 
+@pytest.mark.parametrize("C", [1, 3, 4])
+def test_remap_tile_paths(tsm, oracle, C):
+    """The LDS-tiled fixed-map kernel: tiles whose source window fits the LDS stage (smooth
+    warp), tiles that do not (scattered maps: the direct per-pixel path inside the tile),
+    both in one map, and a source at a 1-byte offset (the untiled kernel)."""
+    import torch
+
+    rng = np.random.default_rng(31 + C)
+    H, W, sh, sw = 70, 300, 64, 290
+    src = rng.integers(0, 256, (sh, sw, C) if C > 1 else (sh, sw), dtype=np.uint8)
+    _, _, xy, fxy = _maps(rng, H, W, sh, sw)
+    # rows 16..31 scattered over (and past) the whole image: no tile window fits
+    xy[16:32, :, 0] = rng.integers(-10, sw + 10, (16, W))
+    xy[16:32, :, 1] = rng.integers(-10, sh + 10, (16, W))
+    want = oracle.remap_linear_fixed(src, xy, fxy)
+    assert np.array_equal(tsm.remap(src, xy, fxy), want)
+    big = torch.empty(src.size + 1, dtype=torch.uint8, device="cuda")
+    mis = big[1:].view(src.shape)
+    mis.copy_(torch.from_numpy(src).cuda())
+    assert mis.data_ptr() % 4 == 1
+    got = tsm.remap(mis, torch.from_numpy(xy).cuda(), torch.from_numpy(fxy.view(np.int16)).cuda())
+    assert np.array_equal(got.cpu().numpy(), want)
+
+
 def test_remap_float_map_edge_values(tsm, oracle):
     rng = np.random.default_rng(4)
     src = rng.integers(0, 256, (30, 40, 3), dtype=np.uint8)

@@ -1,14 +1,19 @@
 #!/usr/bin/env python3
 """Per-kernel HBM bytes per dispatch from two rocprofv3 --pmc passes (FETCH_SIZE, WRITE_SIZE),
-config B single-pair launches, against each kernel's algorithmic bytes.
-FETCH_SIZE is doubled (gfx950 tallies 64 B per 128-B request, MI355X_MICROARCH.md)."""
+single-pair launches, against each kernel's algorithmic bytes.
+FETCH_SIZE is doubled (gfx950 tallies 64 B per 128-B request, MI355X_MICROARCH.md).
+
+    pmc_all.py fetch.csv write.csv [H W L label]      (default: config B, 375 1242 193)"""
 import collections
 import csv
 import json
 import sys
 
-L, N = 193, 1242 * 375
-VOL = 2 * L * N * 4  # the two-view volume, one pair
+H, W, L = (int(x) for x in sys.argv[3:6]) if len(sys.argv) >= 6 else (375, 1242, 193)
+LABEL = sys.argv[6] if len(sys.argv) >= 7 else "config B (synthetic)"
+LP = (L + 3) // 4 * 4
+N = H * W
+VOL = 2 * LP * N * 4  # the two-view volume at the padded stride, one pair
 
 
 def per(path, counter):
@@ -41,8 +46,12 @@ def algorithmic(n):
 
 
 f, w = per(sys.argv[1], "FETCH_SIZE"), per(sys.argv[2], "WRITE_SIZE")
-out = {"note": "bytes per dispatch; FETCH_SIZE x2 (gfx950); single-pair launches of config B; "
-               "scanline passes store only changed vectors, so their write is below the algorithmic bound",
+out = {"note": f"bytes per dispatch; FETCH_SIZE x2 (gfx950); single-pair launches of {LABEL} "
+               f"({W}x{H}, {L} labels); a scanline pass leaves a pixel untouched when its predecessor's "
+               "minimum is exactly 0 (ADCensus.cpp:880-881) and then does not store it: exact-shift "
+               "synthetic pairs have many such pixels, noisy and real pairs none, so on synthetic pairs "
+               "the scanline's write is below the algorithmic bound",
+       "workload": {"H": H, "W": W, "L": L, "label": LABEL},
        "kernels": {}}
 for n in sorted(set(f) | set(w)):
     fb = 2 * sum(f[n]) / len(f[n]) if f.get(n) else None

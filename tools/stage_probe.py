@@ -29,11 +29,29 @@ def main():
     ap.add_argument("--pairs", type=int, default=16)
     ap.add_argument("--concurrency", type=int, default=8)
     ap.add_argument("--label", default=os.environ.get("TSM_EXPERIMENT_LIB", "default"))
+    ap.add_argument("--png", nargs=2, default=None, help="a real pair (tests/golden/demo names), replicated")
+    ap.add_argument("--noisy", action="store_true", help="config-B style pairs with +-3 noise on the right view")
+    ap.add_argument("--grey", action="store_true", help="grey synthetic scenes (config E)")
+    ap.add_argument("--single", type=int, default=0, help="also time N single-frame compute() calls")
     a = ap.parse_args()
-    H, W, D, n = a.height, a.width, a.max_disparity, a.pairs
+    D, n = a.max_disparity, a.pairs
     dev = torch.device("cuda", 0)
     lefts, rights = [], []
-    for l, r, _ in tsm.synthetic.make_scene_batch([1000 + i for i in range(n)], H, W, D + 1, threads=16):
+    if a.png:
+        import numpy as np
+        from PIL import Image
+
+        d = os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", "tests", "golden", "demo")
+        ld = lambda f: np.ascontiguousarray(np.array(Image.open(os.path.join(d, f)).convert("RGB"))[:, :, ::-1])  # noqa: E731
+        l0, r0 = ld(a.png[0]), ld(a.png[1])
+        pairs = [(l0, r0, None)] * n
+    elif a.noisy:
+        pairs = [tsm.synthetic.config_b_noisy(1000 + i) for i in range(n)]
+    else:
+        pairs = tsm.synthetic.make_scene_batch([1000 + i for i in range(n)], a.height, a.width, D + 1, threads=16,
+                                               grayscale=a.grey)
+    H, W = pairs[0][0].shape[:2]
+    for l, r, _ in pairs:
         lefts.append(torch.from_numpy(l).to(dev))
         rights.append(torch.from_numpy(r).to(dev))
     outs = torch.empty((n, H, W), dtype=torch.float32, device=dev)
@@ -54,6 +72,15 @@ def main():
     torch.cuda.synchronize()
     pps = 2 * n / (time.perf_counter() - t0)
     m.setConcurrency(1)
+    single = None
+    if a.single:
+        m.compute_device_ptr(lp[0], rp[0], H, W, W * 3, op[0], W * 4)
+        m.synchronize()
+        t1 = time.perf_counter()
+        for i in range(a.single):
+            m.compute_device_ptr(lp[i % n], rp[i % n], H, W, W * 3, op[i % n], W * 4)
+            m.synchronize()
+        single = round((time.perf_counter() - t1) / a.single * 1e3, 3)
     m.setProfiling(True)
     m.resetStageTimes()
     k = min(n, 8)
@@ -61,7 +88,7 @@ def main():
     torch.cuda.synchronize()
     st = m.stageTimes()
     m.close()
-    print(a.label, f"{W}x{H} D={D}{' HSI' if a.hsi else ''}", round(pps, 2),
+    print(a.label, f"{W}x{H} D={D}{' HSI' if a.hsi else ''}", round(pps, 2), f"single_ms={single}",
           json.dumps({kk: round(v[0] / max(1, v[1]), 4) for kk, v in st.items()}), flush=True)
 
 
