@@ -145,10 +145,12 @@ __global__ void k_oscan_count(const int32_t* __restrict__ disp, int n, int minD,
 // Each block's first rank is the sum of the outlier counts of the blocks before it (read
 // and reduced here: a few hundred counts, no separate scan launch); the last block writes
 // the total.
+// rank[p] = the outliers before pixel p in raster order (rank[n] = all of them): the valid
+// pixels of a raster range [p0, p1] are then (p1 - p0 + 1) - (rank[p1 + 1] - rank[p0]).
 __global__ void k_oscan_scatter(const int32_t* __restrict__ disp, int n, int minD, const int32_t* __restrict__ bsum,
                                 int32_t* __restrict__ out_list, int32_t* __restrict__ dtmp,
-                                int32_t* __restrict__ counts, size_t ps) {
-    pair_shift(blockIdx.z, ps, disp, bsum, out_list, dtmp, counts);
+                                int32_t* __restrict__ counts, int32_t* __restrict__ rank, size_t ps) {
+    pair_shift(blockIdx.z, ps, disp, bsum, out_list, dtmp, counts, rank);
     __shared__ int s_base;
     if (threadIdx.x == 0) s_base = 0;
     __syncthreads();
@@ -171,6 +173,15 @@ __global__ void k_oscan_scatter(const int32_t* __restrict__ disp, int n, int min
         counts[0] = first + sa[SC_THREADS - 1];
         counts[1] = 0;
         counts[2] = 0;  // the decision's long-carry list (k_vote_decide_wave)
+        rank[n] = first + sa[SC_THREADS - 1];
+    }
+    {
+        int rk = a;
+#pragma unroll
+        for (int k = 0; k < SC_ITEMS; ++k) {
+            if (base + k < n) rank[base + k] = rk;
+            rk += dv[k] < minD ? 1 : 0;
+        }
     }
     if (base + SC_ITEMS <= n) {
 #pragma unroll
@@ -184,48 +195,18 @@ __global__ void k_oscan_scatter(const int32_t* __restrict__ disp, int n, int min
         if (dv[k] < minD) out_list[a++] = base + k;
 }
 
-// Valid-pixel prefix counts along the inner direction of a voting pass (valid: disp >= minD,
-// the reference's sample test :1122): the vote of a row segment is then the difference of
-// two prefix entries, exact integer arithmetic in any order.
-//   rows (hf):     pre[y (W+1) + x] = valid pixels of row y at columns < x, x in [0, W]
-//   columns (!hf): P(y, x) = cpre[(y >> 5) W + x] + pre[y W + x], the valid pixels of column x
-//                  at rows < y (y in [0, H]): pre holds the count inside 32-row chunks, cpre
-//                  the counts of the chunks before (two launches, W x H/32 threads)
+// Valid-pixel counts of a voting pass's inner segments (valid: disp >= minD, the
+// reference's sample test :1122) as differences of prefix counts, exact integer arithmetic in
+// any order.  Rows (hf): the raster ranks of k_oscan_scatter.  Columns (!hf):
+//   P(y, x) = cpre[(y >> 5) W + x] + pre[y W + x], the valid pixels of column x at rows < y
+//   (y in [0, H]): pre holds the count inside 32-row chunks, cpre the counts of the chunks
+//   before (two launches, W x H/32 threads).
+// vpre: rank[0 .. N], then pre[(H+1) W], then cpre[(H/32+2) W].
 constexpr int VP_CH = 32;
 size_t refine_vpre_ints(int H, int W) {
-    const size_t r = (size_t)H * (W + 1), c = (size_t)(H + 1) * W + (size_t)(H / VP_CH + 2) * W;
-    return r > c ? r : c;
+    return (size_t)H * W + 1 + (size_t)(H + 1) * W + (size_t)(H / VP_CH + 2) * W;
 }
-
-__global__ __launch_bounds__(256) void k_vprefix_rows(const int32_t* __restrict__ disp, int32_t* __restrict__ pre,
-                                                      DevParams Pk) {
-    const DevParams P = Pk;
-    pair_shift(blockIdx.z, P.pstride, disp, pre);
-    __shared__ int s_w[4];
-    const int W = P.W, y = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
-    const int32_t* row = disp + (size_t)y * W;
-    int32_t* out = pre + (size_t)y * (W + 1);
-    int carry = 0;
-    for (int x0 = 0; x0 < W; x0 += 256) {
-        const int x = x0 + tid;
-        const int v = x < W && row[x] >= P.minD ? 1 : 0;
-        int incl = v;
-#pragma unroll
-        for (int d = 1; d < 64; d <<= 1) {
-            const int t = __shfl_up(incl, d);
-            if (lane >= d) incl += t;
-        }
-        if (lane == 63) s_w[wv] = incl;
-        __syncthreads();
-        int before = carry;
-        for (int k = 0; k < wv; ++k) before += s_w[k];
-        if (x < W) out[x] = before + incl - v;
-        const int tot = s_w[0] + s_w[1] + s_w[2] + s_w[3];
-        __syncthreads();
-        carry += tot;
-    }
-    if (tid == 0) out[W] = carry;
-}
+__host__ __device__ inline size_t vpre_cols_off(int H, int W) { return (size_t)H * W + 1; }
 
 // columns, step 1: thread (chunk c, column x) counts inside rows [32c, 32c + 32); the chunk
 // holding row H also writes P's local part at y = H
@@ -234,6 +215,7 @@ __global__ __launch_bounds__(256) void k_vprefix_cols(const int32_t* __restrict_
     const DevParams P = Pk;
     pair_shift(blockIdx.z, P.pstride, disp, pre);
     const int W = P.W, H = P.H;
+    pre += vpre_cols_off(H, W);
     const int x = blockIdx.x * 256 + threadIdx.x, c = blockIdx.y;
     if (x >= W) return;
     int32_t* cpre = pre + (size_t)(H + 1) * W;
@@ -257,6 +239,7 @@ __global__ __launch_bounds__(256) void k_vprefix_cols_scan(int32_t* __restrict__
     const DevParams P = Pk;
     pair_shift(blockIdx.z, P.pstride, pre);
     const int W = P.W, H = P.H;
+    pre += vpre_cols_off(H, W);
     const int x = blockIdx.x * 256 + threadIdx.x;
     if (x >= W) return;
     int32_t* cpre = pre + (size_t)(H + 1) * W;
@@ -272,10 +255,11 @@ __global__ __launch_bounds__(256) void k_vprefix_cols_scan(int32_t* __restrict__
 // valid pixels of the inner segment at (yy0, xx0), offsets [-a2, b2] along the inner direction
 __device__ __forceinline__ int seg_votes(const int32_t* __restrict__ pre, bool hf, int H, int W, int yy0, int xx0,
                                          int a2, int b2) {
-    if (hf) {
-        const int32_t* pr = pre + (size_t)yy0 * (W + 1);
-        return pr[xx0 + b2 + 1] - pr[xx0 - a2];
+    if (hf) {  // raster ranks: the segment is the raster range [p0, p1]
+        const size_t p0 = (size_t)yy0 * W + xx0 - a2, p1 = (size_t)yy0 * W + xx0 + b2;
+        return (a2 + b2 + 1) - (pre[p1 + 1] - pre[p0]);
     }
+    pre += vpre_cols_off(H, W);
     const int32_t* cpre = pre + (size_t)(H + 1) * W;
     const int ya = yy0 - a2, yb = yy0 + b2 + 1;
     return cpre[(size_t)(yb / VP_CH) * W + xx0] + pre[(size_t)yb * W + xx0] -
@@ -420,7 +404,7 @@ __global__ void k_hv_scatter(const int32_t* __restrict__ cvote, int32_t* __restr
 // argmax and the ratio test (:1137-1153).  No workgroup barrier: every wave is independent.
 constexpr int VD_WAVES = 4;
 constexpr int VD_CB = 8;      // carried votes loaded a lane per round trip (512 ranks a wave)
-constexpr int VD_LONG = 2048; // carries longer than this go to k_vote_decide_long (a workgroup a rank)
+constexpr int VD_LONG = 512;  // carries longer than this go to k_vote_decide_long (a workgroup a rank)
 __global__ __launch_bounds__(VD_WAVES * 64) void k_vote_decide_wave(
     const int32_t* __restrict__ disp, int32_t* __restrict__ dtmp, const uint32_t* __restrict__ arms,
     const int32_t* __restrict__ out_list, const int32_t* __restrict__ cvote, const uint16_t* __restrict__ csamp,
@@ -544,9 +528,13 @@ __global__ __launch_bounds__(VL_THREADS) void k_vote_decide_long(
             region_arms(arms[(size_t)yy0 * W + xx0], hf, a1, b1, a2, b2);
             const ptrdiff_t st = hf ? 1 : W;
             const int32_t* rp = disp + (size_t)yy0 * W + xx0;
-            for (int ii = -a2; ii <= b2; ++ii) {
-                const int d = rp[(ptrdiff_t)ii * st];
-                if (d >= minD) atomicAdd(&hist[d - minD], 1);
+            for (int ii = -a2; ii <= b2; ii += RW_B) {  // RW_B loads a round trip
+                int dv[RW_B];
+#pragma unroll
+                for (int kk = 0; kk < RW_B; ++kk) dv[kk] = ii + kk <= b2 ? rp[(ptrdiff_t)(ii + kk) * st] : -1;
+#pragma unroll
+                for (int kk = 0; kk < RW_B; ++kk)
+                    if (dv[kk] >= minD) atomicAdd(&hist[dv[kk] - minD], 1);
             }
         }
         for (int kb = prev + 1; kb < r; kb += VD_CB * VL_THREADS) {
@@ -1084,12 +1072,9 @@ void launch_region_voting(RefineBufs& B, const uint32_t* arms0, int hf, const De
     hipLaunchKernelGGL(k_oscan_count, grid1d(nb, P), dim3(SC_THREADS), 0, st, B.dm, n, P.minD, B.bsum, ps);
     trace_point("k_oscan_count", st);
     hipLaunchKernelGGL(k_oscan_scatter, grid1d(nb, P), dim3(SC_THREADS), 0, st, B.dm, n, P.minD, B.bsum,
-                       B.out_list, B.dtmp, B.counts, ps);
+                       B.out_list, B.dtmp, B.counts, B.vpre, ps);
     trace_point("k_oscan_scatter", st);
-    if (hf) {
-        hipLaunchKernelGGL(k_vprefix_rows, grid1d(P.H, P), dim3(256), 0, st, B.dm, B.vpre, P);
-        trace_point("k_vprefix_rows", st);
-    } else {
+    if (!hf) {  // vertical inner segments: column prefix counts (rows use the raster ranks)
         hipLaunchKernelGGL(k_vprefix_cols, dim3((P.W + 255) / 256, P.H / VP_CH + 1, P.npairs), dim3(256), 0, st,
                            B.dm, B.vpre, P);
         hipLaunchKernelGGL(k_vprefix_cols_scan, dim3((P.W + 255) / 256, 1, P.npairs), dim3(256), 0, st, B.vpre, P);

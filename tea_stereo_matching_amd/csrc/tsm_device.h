@@ -204,6 +204,11 @@ __device__ __forceinline__ uint64_t wave_min_u64(uint64_t v) {
     return v;
 }
 
+__device__ __forceinline__ int wave_max_i32(int v) {
+    for (int off = 32; off >= 1; off >>= 1) v = max(v, __shfl_xor(v, off));
+    return v;
+}
+
 __device__ __forceinline__ int wave_sum_i(int v) {
     for (int off = 32; off >= 1; off >>= 1) v += __shfl_xor(v, off);
     return v;

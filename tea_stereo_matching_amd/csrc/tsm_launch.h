@@ -85,7 +85,7 @@ struct RefineBufs {
     float* subpix;    // [H][W]
     int32_t* vpre;    // valid-pixel prefix counts of a voting pass (refine_vpre_ints)
 };
-// ints of RefineBufs.vpre: rows (H x (W+1)) or columns ((H+1) x W + chunk prefixes)
+// ints of RefineBufs.vpre: raster ranks (H W + 1), column prefixes ((H+1) W + chunk prefixes)
 size_t refine_vpre_ints(int H, int W);
 size_t refine_scan_blocks(int n);
 void launch_outlier(RefineBufs& B, const DevParams& P, hipStream_t st);
