@@ -600,7 +600,8 @@ def ops_leg(tsm, outs, lefts, H, W, iters=50):
     on the library's null stream, then one synchronize; us = wall time / iters.
     Algorithmic bytes per call: colour map 11 B/px (disparity read by the min/max and
     the LUT pass, 3 B written), depth 8, points 16, remap (BGR, fixed maps) 12: 6 B of
-    map, 3 B of source, 3 B written."""
+    map, 3 B of source, 3 B written (the group remap: the maps once, 6 B a pixel, plus
+    6 B a pixel per image)."""
     import ctypes
 
     import numpy as np
@@ -671,7 +672,9 @@ def ops_leg(tsm, outs, lefts, H, W, iters=50):
         us = timed(fn, iters)
         gbs = bpp * N / (us * 1e-6) / 1e9
         gus = timed(group[name], max(4, iters // 10))
-        ggbs = bpp * N * G / (gus * 1e-6) / 1e9
+        # the group remap reads its one pair of maps (6 B a pixel) once for the G images
+        gbytes = (6 * N + 6 * N * G) if name == "f4_remap" else bpp * N * G
+        ggbs = gbytes / (gus * 1e-6) / 1e9
         res[name] = {"us": round(us, 2), "bytes_per_px": bpp, "GBps": round(gbs, 1),
                      "frac": round(gbs / HBM_PEAK_GBS, 4),
                      f"group{G}": {"us_per_call": round(gus, 1), "us_per_map": round(gus / G, 2),

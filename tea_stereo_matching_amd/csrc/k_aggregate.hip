@@ -233,6 +233,7 @@ struct AggStream {
     int nlv;               // lines per view
     int nl;                // lines of both views
     uint32_t* err;         // CHK: the trace flag (trace_flag())
+    int slices_x;          // > 1: the label slices interleaved along blockIdx.x (see k_agg_split)
 };
 
 constexpr int AX_MIR = 3;  // mirror slots after each ring (a 4-read block spans 3 slots past its start)
@@ -290,7 +291,11 @@ __global__ __launch_bounds__(AX_THREADS) void k_agg_split(AggStream S, DevParams
     pair_shift(blockIdx.z, P.pstride, S.vol, S.arms, S.ws, S.pk, S.rcp);
     extern __shared__ __attribute__((aligned(16))) f32x4 smem_f4[];
     const int H = P.H, W = P.W, Lp = P.Lp;
-    const int slice = blockIdx.y;
+    // label slices: when the grid interleaves them (slices_x > 1), the slices of one line group
+    // are blocks 8 apart (same XCD) and dispatched together, so the 64-B granules two slices'
+    // pieces of a pixel vector share are fetched once into that XCD's L2
+    const int nsx = S.slices_x;
+    const int slice = nsx > 1 ? (int)((blockIdx.x >> 3) % nsx) : (int)blockIdx.y;
     const int Q = QT > 0 ? QT : min(S.qn0, S.qtot - slice * S.qn0);
     float* const volq = S.vol + 4 * slice * S.qn0;  // this slice's first label
     const uint32_t Qs = (uint32_t)Q * 16;                                // bytes per ring pixel
@@ -299,7 +304,9 @@ __global__ __launch_bounds__(AX_THREADS) void k_agg_split(AggStream S, DevParams
     const size_t ls = S.horizontal ? (size_t)W * Lp : (size_t)Lp;          // floats per line step
     const uint32_t aes = S.horizontal ? 1u : (uint32_t)W;
     const uint32_t als = S.horizontal ? (uint32_t)W : 1u;
-    const int g = xcd_remap(blockIdx.x, gridDim.x), G = gridDim.x;
+    const int G = gridDim.x / nsx;
+    const int g = nsx > 1 ? (int)(blockIdx.x & 7) * (G >> 3) + (int)((blockIdx.x >> 3) / nsx)
+                          : xcd_remap(blockIdx.x, gridDim.x);
     const int my_lines = (S.nl - g + G - 1) / G;
     const int nch = my_lines * S.cpl;
     const uint32_t r1_off = 0;                                            // LDS byte offsets
@@ -666,7 +673,12 @@ int launch_aggregation_pass(float* vol, const uint32_t* arms, const int32_t* ws,
     // every pass through the role-split streamer (round 4, same box: 409 against 406.5
     // pairs/s with the single passes on the former loader/summer streamer)
     const size_t slds = agg_split_lds(S.qn0);
-    const dim3 sgrid(G, nslice, P.npairs);
+    // several slices: interleaved along x, G / nslice line groups (a multiple of 8: one per XCD
+    // slot), each slice of a group on the same XCD at the same time
+    int Gs = (ncu / nslice) & ~7;
+    if (Gs > S.nl) Gs = S.nl & ~7;
+    S.slices_x = (nslice > 1 && Gs >= 8) ? nslice : 1;
+    const dim3 sgrid = S.slices_x > 1 ? dim3(Gs * nslice, 1, P.npairs) : dim3(G, nslice, P.npairs);
     if (fused) {
         if (big) launch_split_t<true, 0, true>(S, P, sgrid, slds, st);
         else if (Q == 49 && nslice == 1) launch_split_t<true, 49, false>(S, P, sgrid, slds, st);

@@ -472,19 +472,41 @@ __device__ __forceinline__ void lds_taps(const uint32_t* __restrict__ box, int p
     }
 }
 
-__device__ __forceinline__ int block_reduce(int v, bool mx, int* red, int slot) {
-#pragma unroll
-    for (int s = 32; s >= 1; s >>= 1) {
-        const int o = __shfl_xor(v, s);
-        v = mx ? max(v, o) : min(v, o);
+// The source window of every tile, once per call (the maps are shared by all the call's
+// images): box[t] = (x0, x1, y0, y1) of the taps of tile t's outputs, clamped to the image
+// (x0 > x1 or y0 > y1: no tap inside).  One workgroup a tile, one combined reduction.
+__global__ __launch_bounds__(OPS_THREADS) void k_remap_boxes(const int16_t* __restrict__ xy, size_t xy_step_e,
+                                                             int rows, int cols, int sh, int sw,
+                                                             int4* __restrict__ boxes) {
+    __shared__ int red[4][OPS_THREADS / 64];
+    const int y = blockIdx.y * RT_ROWS + (int)threadIdx.x / RT_TX;
+    const int x0 = blockIdx.x * RT_COLS + ((int)threadIdx.x % RT_TX) * OPS_PX;
+    const int n = (y < rows && x0 < cols) ? min(OPS_PX, cols - x0) : 0;
+    // reduce (min x, -max x, min y, -max y): all four as minima
+    int v[4] = {0x7fffffff, 0x7fffffff, 0x7fffffff, 0x7fffffff};
+    const int16_t* xr = xy + (size_t)y * xy_step_e + 2 * (size_t)x0;
+    for (int k = 0; k < n; ++k) {
+        const int sx = xr[2 * k], sy = xr[2 * k + 1];
+        v[0] = min(v[0], sx); v[1] = min(v[1], -(sx + 1));
+        v[2] = min(v[2], sy); v[3] = min(v[3], -(sy + 1));
     }
-    const int wv = threadIdx.x >> 6;
-    if ((threadIdx.x & 63) == 0) red[slot * 4 + wv] = v;
-    __syncthreads();
-    int r = red[slot * 4];
 #pragma unroll
-    for (int k = 1; k < OPS_THREADS / 64; ++k) r = mx ? max(r, red[slot * 4 + k]) : min(r, red[slot * 4 + k]);
-    return r;
+    for (int c = 0; c < 4; ++c) {
+#pragma unroll
+        for (int o = 32; o >= 1; o >>= 1) v[c] = min(v[c], __shfl_xor(v[c], o));
+        if ((threadIdx.x & 63) == 0) red[c][threadIdx.x >> 6] = v[c];
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        int r[4];
+#pragma unroll
+        for (int c = 0; c < 4; ++c) {
+            r[c] = red[c][0];
+            for (int w = 1; w < OPS_THREADS / 64; ++w) r[c] = min(r[c], red[c][w]);
+        }
+        boxes[blockIdx.y * gridDim.x + blockIdx.x] = make_int4(max(r[0], 0), min(-r[1], sw - 1), max(r[2], 0),
+                                                              min(-r[3], sh - 1));
+    }
 }
 
 // src must be 4-B aligned with a row step that is a multiple of 4 (the launcher checks):
@@ -493,11 +515,13 @@ template <int C>
 __global__ __launch_bounds__(OPS_THREADS) void k_remap_tile(Tab<const uint8_t> srcs, int sh, int sw, size_t sstep,
                                                             const int16_t* __restrict__ xy, size_t xy_step_e,
                                                             const uint16_t* __restrict__ fxy, size_t fxy_step_e,
-                                                            int rows, int cols, Tab<uint8_t> dsts, size_t dstep) {
+                                                            int rows, int cols, const int4* __restrict__ boxes,
+                                                            Tab<uint8_t> dsts, size_t dstep) {
     __shared__ uint32_t box[RT_LDS_DW];
-    __shared__ int red[4 * (OPS_THREADS / 64)];
     const uint8_t* __restrict__ src = srcs.p[blockIdx.z];
     uint8_t* __restrict__ dst = dsts.p[blockIdx.z];
+    const int4 bb = boxes[blockIdx.y * gridDim.x + blockIdx.x];
+    const int bx0 = bb.x, bx1 = bb.y, by0 = bb.z, by1 = bb.w;
     const int y = blockIdx.y * RT_ROWS + (int)threadIdx.x / RT_TX;
     const int x0 = blockIdx.x * RT_COLS + ((int)threadIdx.x % RT_TX) * OPS_PX;
     const int n = (y < rows && x0 < cols) ? min(OPS_PX, cols - x0) : 0;
@@ -519,18 +543,6 @@ __global__ __launch_bounds__(OPS_THREADS) void k_remap_tile(Tab<const uint8_t> s
             }
         }
     }
-    // bounding box of the tile's taps (x .. x+1, y .. y+1), clamped to the image
-    int lx = 0x7fffffff, hx = -0x7fffffff, ly = 0x7fffffff, hy = -0x7fffffff;
-#pragma unroll
-    for (int k = 0; k < OPS_PX; ++k) {
-        if (k < n) {
-            const int sx = (int)(int16_t)(mxy[k] & 0xffffu), sy = (int)(int16_t)(mxy[k] >> 16);
-            lx = min(lx, sx); hx = max(hx, sx + 1);
-            ly = min(ly, sy); hy = max(hy, sy + 1);
-        }
-    }
-    const int bx0 = max(block_reduce(lx, false, red, 0), 0), bx1 = min(block_reduce(hx, true, red, 1), sw - 1);
-    const int by0 = max(block_reduce(ly, false, red, 2), 0), by1 = min(block_reduce(hy, true, red, 3), sh - 1);
     const int cb0 = (bx0 * C) & ~3;                              // first staged byte of a row
     const int pitch_dw = ((bx1 + 1) * C - cb0 + 3) / 4 + 1;     // + 1: the 3-dword tap reads
     const int nbr = by1 - by0 + 1;
@@ -937,21 +949,30 @@ int tsm_remap_linear_fixed_batch_device(int n, const uint8_t* const* d_srcs, int
     // the LDS-tiled form when every source row starts on a dword (the usual case)
     bool aligned = src_step % 4 == 0;
     for (int i = 0; i < n && aligned; ++i) aligned = ((uintptr_t)d_srcs[i] & 3) == 0;
-    if (aligned) {
+    if (aligned && n > 0) {
+        // the tiles' source windows once for the call (stream-ordered scratch), then the tiles
+        const dim3 gt((cols + RT_COLS - 1) / RT_COLS, (rows + RT_ROWS - 1) / RT_ROWS, 1);
+        int4* boxes = nullptr;
+        hipError_t e = hipMallocAsync((void**)&boxes, (size_t)gt.x * gt.y * sizeof(int4), st);
+        if (e != hipSuccess) return status(e);
+        hipLaunchKernelGGL(k_remap_boxes, gt, dim3(OPS_THREADS), 0, st, d_xy, xy_step / 2, rows, cols, src_rows,
+                           src_cols, boxes);
         for (int i = 0; i < n; i += kOpsBatch) {
             const int k = min(kOpsBatch, n - i);
-            const dim3 g((cols + RT_COLS - 1) / RT_COLS, (rows + RT_ROWS - 1) / RT_ROWS, k);
+            const dim3 g(gt.x, gt.y, k);
             const Tab<const uint8_t> s = tab_of<const uint8_t>(d_srcs + i, k);
             const Tab<uint8_t> d = tab_of<uint8_t>(d_dsts + i, k);
 #define TSM_REMAP_TILE(CC)                                                                               \
             hipLaunchKernelGGL(k_remap_tile<CC>, g, dim3(OPS_THREADS), 0, st, s, src_rows, src_cols, src_step, \
-                               d_xy, xy_step / 2, d_fxy, fxy_step / 2, rows, cols, d, dst_step)
+                               d_xy, xy_step / 2, d_fxy, fxy_step / 2, rows, cols, boxes, d, dst_step)
             if (C == 1) TSM_REMAP_TILE(1);
             else if (C == 3) TSM_REMAP_TILE(3);
             else TSM_REMAP_TILE(4);
 #undef TSM_REMAP_TILE
         }
-        return status(hipGetLastError());
+        e = hipGetLastError();
+        const hipError_t f = hipFreeAsync(boxes, st);
+        return status(e != hipSuccess ? e : f);
     }
     // packed maps and output run as one row (the source is addressed through the maps)
     const bool dense = xy_step == 4 * (size_t)cols && fxy_step == 2 * (size_t)cols && dst_step == (size_t)C * cols &&
