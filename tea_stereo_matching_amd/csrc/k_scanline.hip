@@ -140,6 +140,9 @@ __device__ __forceinline__ int vec_argmin_nb(const f32x4 (&x)[J], int lane, int 
 
 // Hot-loop scalars, pinned in SGPRs (an empty asm makes each value opaque, so the
 // compiler cannot rematerialise it from kernarg memory inside the serial loop).
+// The six P1 / P2 values live in VGPRs (loop-invariant copies): a step's per-label selects
+// (v_cndmask with a lane-mask SGPR pair) may read only one scalar operand, so scalar copies
+// would be moved to VGPRs again at every step.
 struct ScanConst {
     int L, Q, cd, minD, W, gstride, gpad;
     float p1[3], p2[3];
@@ -148,7 +151,11 @@ __device__ __forceinline__ ScanConst scan_const(const DevParams& P) {
     ScanConst c{P.L, P.Lp >> 2, P.color_diff, P.minD, P.W, P.gstride, P.gpad,
                 {P.p1t[0], P.p1t[1], P.p1t[2]}, {P.p2t[0], P.p2t[1], P.p2t[2]}};
     asm volatile("" : "+s"(c.L), "+s"(c.Q), "+s"(c.cd), "+s"(c.minD), "+s"(c.W), "+s"(c.gstride), "+s"(c.gpad));
-    asm volatile("" : "+s"(c.p1[0]), "+s"(c.p1[1]), "+s"(c.p1[2]), "+s"(c.p2[0]), "+s"(c.p2[1]), "+s"(c.p2[2]));
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+        asm volatile("v_mov_b32 %0, %1" : "=v"(c.p1[k]) : "s"(P.p1t[k]));
+        asm volatile("v_mov_b32 %0, %1" : "=v"(c.p2[k]) : "s"(P.p2t[k]));
+    }
     return c;
 }
 
@@ -495,13 +502,14 @@ __global__ __launch_bounds__(HELP ? 2 * SH_LINES * 64 : 256) void k_scan_line(fl
         // would keep the slot's registers live past the refill, and the compiler would then
         // rotate the whole ring by copies at the loop back-edge (each copy waiting for its
         // in-flight load: the prefetch gone)
+        // the select itself writes q's registers (early clobber): no separate copy
+        const uint64_t umask = __builtin_amdgcn_ballot_w64(upd);
 #pragma unroll
         for (int j = 0; j < J; ++j) {
-            const f32x4 sel = upd ? np[j] : s.p[j];
 #pragma unroll
             for (int e = 0; e < 4; ++e) {
                 float o;
-                asm volatile("v_mov_b32 %0, %1" : "=&v"(o) : "v"(sel[e]));
+                asm volatile("v_cndmask_b32_e64 %0, %1, %2, %3" : "=&v"(o) : "v"(s.p[j][e]), "v"(np[j][e]), "s"(umask));
                 q[j][e] = o;
             }
         }
