@@ -15,6 +15,7 @@
 
 #include <map>
 #include <mutex>
+#include <type_traits>
 #include <utility>
 
 #include "tsm_adcensus.h"
@@ -45,12 +46,12 @@ struct Grp {
     int y, x0, n;  // row, first pixel, pixels in the group (0: past the map)
 };
 __device__ __forceinline__ Grp pixel_group(int rows, int cols) {
-    const int gpr = (cols + OPS_PX - 1) / OPS_PX;
-    const long t = (long)blockIdx.x * blockDim.x + threadIdx.x;
-    if (t >= (long)rows * gpr) return Grp{0, 0, 0};
-    const int y = (int)(t / gpr);
-    const int x0 = (int)(t - (long)y * gpr) * OPS_PX;
-    return Grp{y, x0, min(OPS_PX, cols - x0)};
+    const uint32_t gpr = (uint32_t)(cols + OPS_PX - 1) / OPS_PX;
+    const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;  // grids stay below 2^32 threads
+    if ((long)t >= (long)rows * gpr) return Grp{0, 0, 0};
+    const uint32_t y = rows == 1 ? 0u : t / gpr;  // dense maps run as one row: no division
+    const int x0 = (int)(t - y * gpr) * OPS_PX;
+    return Grp{(int)y, x0, min(OPS_PX, cols - x0)};
 }
 
 typedef float f2v __attribute__((ext_vector_type(2)));
@@ -369,7 +370,8 @@ __device__ __forceinline__ void remap_px(const uint8_t* __restrict__ src, int sh
     row_taps<C>(src, sh, sw, sstep, sx, sy + 1, t1);
 #pragma unroll
     for (int c = 0; c < C; ++c)
-        o[c] = (t0[c] * w00 + t0[C + c] * w01 + t1[c] * w10 + t1[C + c] * w11 + (1u << 14)) >> 15;
+        o[c] = (__umul24(t0[c], w00) + __umul24(t0[C + c], w01) + __umul24(t1[c], w10) + __umul24(t1[C + c], w11) +
+                (1u << 14)) >> 15;
 }
 
 template <int C>
@@ -429,163 +431,6 @@ __global__ void k_remap_fixed(Tab<const uint8_t> srcs, int sh, int sw, size_t ss
     store_px<C>(dst + (size_t)p.y * dstep + (size_t)p.x0 * C, n, o);
 }
 
-// Tiled form of k_remap_fixed: rectification maps are near-identity warps, so a tile of
-// RT_ROWS x RT_COLS outputs reads a small source window.  The workgroup reduces its maps'
-// bounding box, stages the box (clamped to the image) in LDS with coalesced dword loads,
-// and every tap is then an LDS read instead of a per-pixel gather through the texture
-// path (two rows x three dwords a pixel).  A box past RT_LDS_DW dwords (arbitrary maps)
-// takes the direct per-pixel path for the whole tile.  Same arithmetic as remap_px.
-constexpr int RT_TX = 32;                      // lanes along a tile row (4 pixels each)
-constexpr int RT_ROWS = OPS_THREADS / RT_TX;   // 8
-constexpr int RT_COLS = RT_TX * OPS_PX;        // 128
-constexpr int RT_LDS_DW = 6144;                // 24 KB of staged source a workgroup
-
-template <int C>
-__device__ __forceinline__ void lds_taps(const uint32_t* __restrict__ box, int pitch_dw, int by0, int cb0,
-                                         int sh, int sw, int sx, int sy, uint32_t (&b)[2 * C]) {
-    if (sy < 0 || sy >= sh) {
-#pragma unroll
-        for (int i = 0; i < 2 * C; ++i) b[i] = 0;
-        return;
-    }
-    const uint32_t* row = box + (sy - by0) * pitch_dw;
-    if (sx >= 0 && sx + 1 < sw) {  // both taps in the image: 2C bytes from <= 3 dwords
-        const int o = sx * C - cb0;
-        const uint32_t* w = row + (o >> 2);
-        const uint32_t w0 = w[0], w1 = w[1], w2 = (2 * C + (o & 3) > 8) ? w[2] : 0u;
-        const uint32_t s8 = (uint32_t)(o & 3) * 8;
-        const uint32_t lo = __builtin_amdgcn_alignbit(w1, w0, s8);
-        const uint32_t hi = __builtin_amdgcn_alignbit(w2, w1, s8);
-#pragma unroll
-        for (int i = 0; i < 2 * C; ++i) b[i] = ((i < 4 ? lo : hi) >> (8 * (i & 3))) & 0xffu;
-        return;
-    }
-#pragma unroll
-    for (int t = 0; t < 2; ++t) {
-        const int x = sx + t;
-        const bool in = x >= 0 && x < sw;
-#pragma unroll
-        for (int c = 0; c < C; ++c) {
-            const int o = x * C + c - cb0;
-            b[t * C + c] = in ? (row[o >> 2] >> (8 * (o & 3))) & 0xffu : 0u;
-        }
-    }
-}
-
-// The source window of every tile, once per call (the maps are shared by all the call's
-// images): box[t] = (x0, x1, y0, y1) of the taps of tile t's outputs, clamped to the image
-// (x0 > x1 or y0 > y1: no tap inside).  One workgroup a tile, one combined reduction.
-__global__ __launch_bounds__(OPS_THREADS) void k_remap_boxes(const int16_t* __restrict__ xy, size_t xy_step_e,
-                                                             int rows, int cols, int sh, int sw,
-                                                             int4* __restrict__ boxes) {
-    __shared__ int red[4][OPS_THREADS / 64];
-    const int y = blockIdx.y * RT_ROWS + (int)threadIdx.x / RT_TX;
-    const int x0 = blockIdx.x * RT_COLS + ((int)threadIdx.x % RT_TX) * OPS_PX;
-    const int n = (y < rows && x0 < cols) ? min(OPS_PX, cols - x0) : 0;
-    // reduce (min x, -max x, min y, -max y): all four as minima
-    int v[4] = {0x7fffffff, 0x7fffffff, 0x7fffffff, 0x7fffffff};
-    const int16_t* xr = xy + (size_t)y * xy_step_e + 2 * (size_t)x0;
-    for (int k = 0; k < n; ++k) {
-        const int sx = xr[2 * k], sy = xr[2 * k + 1];
-        v[0] = min(v[0], sx); v[1] = min(v[1], -(sx + 1));
-        v[2] = min(v[2], sy); v[3] = min(v[3], -(sy + 1));
-    }
-#pragma unroll
-    for (int c = 0; c < 4; ++c) {
-#pragma unroll
-        for (int o = 32; o >= 1; o >>= 1) v[c] = min(v[c], __shfl_xor(v[c], o));
-        if ((threadIdx.x & 63) == 0) red[c][threadIdx.x >> 6] = v[c];
-    }
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        int r[4];
-#pragma unroll
-        for (int c = 0; c < 4; ++c) {
-            r[c] = red[c][0];
-            for (int w = 1; w < OPS_THREADS / 64; ++w) r[c] = min(r[c], red[c][w]);
-        }
-        boxes[blockIdx.y * gridDim.x + blockIdx.x] = make_int4(max(r[0], 0), min(-r[1], sw - 1), max(r[2], 0),
-                                                              min(-r[3], sh - 1));
-    }
-}
-
-// src must be 4-B aligned with a row step that is a multiple of 4 (the launcher checks):
-// then every source row starts on a dword and the staged rows need no per-row shift.
-template <int C>
-__global__ __launch_bounds__(OPS_THREADS) void k_remap_tile(Tab<const uint8_t> srcs, int sh, int sw, size_t sstep,
-                                                            const int16_t* __restrict__ xy, size_t xy_step_e,
-                                                            const uint16_t* __restrict__ fxy, size_t fxy_step_e,
-                                                            int rows, int cols, const int4* __restrict__ boxes,
-                                                            Tab<uint8_t> dsts, size_t dstep) {
-    __shared__ uint32_t box[RT_LDS_DW];
-    const uint8_t* __restrict__ src = srcs.p[blockIdx.z];
-    uint8_t* __restrict__ dst = dsts.p[blockIdx.z];
-    const int4 bb = boxes[blockIdx.y * gridDim.x + blockIdx.x];
-    const int bx0 = bb.x, bx1 = bb.y, by0 = bb.z, by1 = bb.w;
-    const int y = blockIdx.y * RT_ROWS + (int)threadIdx.x / RT_TX;
-    const int x0 = blockIdx.x * RT_COLS + ((int)threadIdx.x % RT_TX) * OPS_PX;
-    const int n = (y < rows && x0 < cols) ? min(OPS_PX, cols - x0) : 0;
-    uint32_t mxy[OPS_PX], mf[OPS_PX];
-    if (n > 0) {
-        const int16_t* xr = xy + (size_t)y * xy_step_e + 2 * (size_t)x0;
-        const uint16_t* fr = fxy + (size_t)y * fxy_step_e + x0;
-        if (n == OPS_PX && ((uintptr_t)xr & 15) == 0 && ((uintptr_t)fr & 7) == 0) {
-            const uint4 a = *reinterpret_cast<const uint4*>(xr);
-            const uint2 b = *reinterpret_cast<const uint2*>(fr);
-            mxy[0] = a.x; mxy[1] = a.y; mxy[2] = a.z; mxy[3] = a.w;
-            mf[0] = b.x; mf[1] = b.x >> 16; mf[2] = b.y; mf[3] = b.y >> 16;
-        } else {
-#pragma unroll
-            for (int k = 0; k < OPS_PX; ++k) {
-                const int kk = k < n ? k : n - 1;
-                mxy[k] = (uint32_t)(uint16_t)xr[2 * kk] | ((uint32_t)(uint16_t)xr[2 * kk + 1] << 16);
-                mf[k] = fr[kk];
-            }
-        }
-    }
-    const int cb0 = (bx0 * C) & ~3;                              // first staged byte of a row
-    const int pitch_dw = ((bx1 + 1) * C - cb0 + 3) / 4 + 1;     // + 1: the 3-dword tap reads
-    const int nbr = by1 - by0 + 1;
-    const bool staged = bx0 <= bx1 && by0 <= by1 && (long)nbr * pitch_dw <= RT_LDS_DW;
-    if (staged) {
-        const size_t end = (size_t)(sh - 1) * sstep + (size_t)sw * C;  // bytes of the image
-        for (int i = threadIdx.x; i < nbr * pitch_dw; i += OPS_THREADS) {
-            const int r = i / pitch_dw, c = i - r * pitch_dw;
-            const size_t off = (size_t)(by0 + r) * sstep + (size_t)cb0 + 4 * (size_t)c;
-            uint32_t v = 0;
-            if (off + 4 <= end) {
-                v = *reinterpret_cast<const uint32_t*>(src + off);
-            } else {
-                for (int k = 0; k < 4; ++k) v |= off + k < end ? (uint32_t)src[off + k] << (8 * k) : 0u;
-            }
-            box[i] = v;
-        }
-        __syncthreads();
-    }
-    if (n == 0) return;
-    uint32_t o[OPS_PX][C];
-#pragma unroll
-    for (int k = 0; k < OPS_PX; ++k) {
-        const int sx = (int)(int16_t)(mxy[k] & 0xffffu);
-        const int sy = (int)(int16_t)(mxy[k] >> 16);
-        const int f = (int)(mf[k] & 1023u);
-        if (staged) {
-            const int fx = f & 31, fy = f >> 5;
-            const uint32_t w00 = (uint32_t)((32 - fx) * (32 - fy) * 32), w01 = (uint32_t)(fx * (32 - fy) * 32);
-            const uint32_t w10 = (uint32_t)((32 - fx) * fy * 32), w11 = (uint32_t)(fx * fy * 32);
-            uint32_t t0[2 * C], t1[2 * C];
-            lds_taps<C>(box, pitch_dw, by0, cb0, sh, sw, sx, sy, t0);
-            lds_taps<C>(box, pitch_dw, by0, cb0, sh, sw, sx, sy + 1, t1);
-#pragma unroll
-            for (int c = 0; c < C; ++c)
-                o[k][c] = (t0[c] * w00 + t0[C + c] * w01 + t1[c] * w10 + t1[C + c] * w11 + (1u << 14)) >> 15;
-        } else {
-            remap_px<C>(src, sh, sw, sstep, sx, sy, f & 31, f >> 5, o[k]);
-        }
-    }
-    store_px<C>(dst + (size_t)y * dstep + (size_t)x0 * C, n, o);
-}
-
 // saturate_cast<int>(v * 32) = cvRound, x86: nearest-even, NaN / out of range -> INT_MIN
 __device__ __forceinline__ int round32(float v) {
     const float a = v * 32.f;
@@ -612,6 +457,219 @@ __global__ void k_remap_float(Tab<const uint8_t> srcs, int sh, int sw, size_t ss
         remap_px<C>(src, sh, sw, sstep, sx, sy, ix & 31, iy & 31, o[k]);
     }
     store_px<C>(dst + (size_t)p.y * dstep + (size_t)p.x0 * C, n, o);
+}
+
+// Buffer form of the remap (sources whose bytes fit 31-bit offsets and row steps < 2^23, the
+// usual case): one code path for every pixel, border taps included, no per-pixel branches.
+//  * the taps of a row come from one 12-B window at the clamped column xw = clamp(sx, 0,
+//    sw-2) of the clamped row, read through a buffer resource whose range check returns 0
+//    for dwords past the image (no read leaves the buffer);
+//  * a tap outside the image (BORDER_CONSTANT 0) gets weight 0 instead of a branch: the
+//    vertical weights (32-fy, fy) of rows outside are 0, and the horizontal weights go to
+//    the window slot that holds the tap's column (sx = -1: tap 1 in slot 0; sx = sw-1:
+//    tap 0 in slot 1) or nowhere;
+//  * per channel the two slots as 16-bit pairs (v_perm of the aligned window), the column
+//    sums v = t0 * wy0 + t1 * wy1 <= 255 * 32 by packed 16-bit multiply-adds, then one
+//    2-term dot product with the horizontal weights.  Exact: sum_ij t_ij w_ij * 32 + 2^14
+//    >> 15 with w = (32-fx | fx) x (32-fy | fy) equals ((32-fx) v0 + fx v1 + 512) >> 10,
+//    and with the horizontal weights scaled by 64 the result is byte 2 of the dot product.
+typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
+typedef uint32_t u32x3v __attribute__((ext_vector_type(3)));
+
+struct RemapSrc {
+    __amdgpu_buffer_rsrc_t r;  // the image's bytes, from the dword holding its first byte
+    uint32_t mis;              // offset of the first byte in that dword
+};
+__device__ __forceinline__ RemapSrc remap_src(const uint8_t* p, uint32_t nbytes) {
+    const uintptr_t u = (uintptr_t)p;
+    const uint32_t mis = (uint32_t)u & 3u;
+    // the dword-rounded range stays in the allocation's last page
+    return RemapSrc{__builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t*>(p - mis), (short)0,
+                                                     (int)((nbytes + mis + 3u) & ~3u), 0x00020000),
+                    mis};
+}
+
+// One pixel's taps, independent of the image (a group of images shares the maps): the two
+// rows' window offsets (without the image's misalignment) and the packed weights.
+struct RemapTap {
+    uint32_t oa, ob;
+    u16x2 vya, vyb, wx;
+};
+// IN: the caller knows every tap of the pixel is inside the image and not in the last row
+// (a wave-uniform test over its lanes' pixels): no clamps, no weight selection.
+template <int C, bool IN>
+__device__ __forceinline__ RemapTap remap_tap(uint32_t sstep, int sh, int sw, int sx, int sy, int fx, int fy) {
+    const int xw = IN ? sx : max(0, min(sx, sw - 2));
+    const int ya = IN ? sy : min(max(sy, 0), sh - 1), yb = IN ? sy + 1 : min(max(sy + 1, 0), sh - 1);
+    const uint32_t cb = __umul24((uint32_t)xw, (uint32_t)C);
+    RemapTap T;
+    T.oa = __umul24((uint32_t)ya, sstep) + cb;
+    T.ob = IN ? T.oa + sstep : __umul24((uint32_t)yb, sstep) + cb;
+    // weights of the two window slots and the two rows (0 for taps outside the image)
+    uint32_t ws0, ws1, wa, wb;
+    if constexpr (IN) {
+        ws0 = (uint32_t)(32 - fx), ws1 = (uint32_t)fx, wa = (uint32_t)(32 - fy), wb = (uint32_t)fy;
+    } else {
+        const int d = sx - xw;  // window slot of tap 0 (tap 1 is in slot d + 1)
+        const bool in0 = (sx >= 0) & (sx < sw), in1 = (sx >= -1) & (sx + 1 < sw);
+        const uint32_t w0 = (uint32_t)(32 - fx), w1 = (uint32_t)fx;
+        ws0 = ((in0 & (d == 0)) ? w0 : 0u) + ((in1 & (d == -1)) ? w1 : 0u);
+        ws1 = ((in0 & (d == 1)) ? w0 : 0u) + ((in1 & (d == 0)) ? w1 : 0u);
+        wa = ((sy >= 0) & (sy < sh)) ? (uint32_t)(32 - fy) : 0u;
+        wb = ((sy >= -1) & (sy + 1 < sh)) ? (uint32_t)fy : 0u;
+    }
+    T.vya = __builtin_bit_cast(u16x2, wa | (wa << 16));
+    T.vyb = __builtin_bit_cast(u16x2, wb | (wb << 16));
+    T.wx = __builtin_bit_cast(u16x2, (ws0 << 6) | (ws1 << 22));
+    return T;
+}
+
+// the pixel of one image: its two windows, the channels' column sums and dot products
+template <int C>
+__device__ __forceinline__ uint32_t remap_apply(const RemapSrc& S, const RemapTap& T) {
+    const uint32_t oa = T.oa + S.mis, ob = T.ob + S.mis;
+    const u32x3v ra = __builtin_amdgcn_raw_buffer_load_b96(S.r, oa & ~3u, 0, 0);
+    const u32x3v rb = __builtin_amdgcn_raw_buffer_load_b96(S.r, ob & ~3u, 0, 0);
+    const uint32_t sa = (oa & 3u) * 8u, sb = (ob & 3u) * 8u;
+    const uint32_t loa = __builtin_amdgcn_alignbit(ra.y, ra.x, sa), hia = __builtin_amdgcn_alignbit(ra.z, ra.y, sa);
+    const uint32_t lob = __builtin_amdgcn_alignbit(rb.y, rb.x, sb), hib = __builtin_amdgcn_alignbit(rb.z, rb.y, sb);
+    uint32_t dc[C];
+#pragma unroll
+    for (int c = 0; c < C; ++c) {
+        // [slot 0 byte c, 0, slot 1 byte C + c, 0]: pool bytes 0-3 = lo, 4-7 = hi
+        constexpr uint32_t z = 0x0c;
+        const uint32_t sel = (uint32_t)c | (z << 8) | ((uint32_t)(C + c) << 16) | (z << 24);
+        const u16x2 ta = __builtin_bit_cast(u16x2, __builtin_amdgcn_perm(hia, loa, sel));
+        const u16x2 tb = __builtin_bit_cast(u16x2, __builtin_amdgcn_perm(hib, lob, sel));
+        const u16x2 v = ta * T.vya + tb * T.vyb;
+        dc[c] = __builtin_amdgcn_udot2(v, T.wx, 512u << 6, false);
+    }
+    // the channels' byte 2s as one packed pixel
+    if constexpr (C == 1) return dc[0] >> 16;
+    const uint32_t p01 = __builtin_amdgcn_perm(dc[1], dc[0], 0x0c0c0602u);
+    if constexpr (C == 3) return (dc[2] & 0xff0000u) | p01;
+    return p01 | __builtin_amdgcn_perm(dc[3], dc[2], 0x06020c0cu);
+}
+
+// 4 packed pixels of C bytes at d: C dwords when whole and aligned
+template <int C>
+__device__ __forceinline__ void store_packed(uint8_t* d, int n, const uint32_t (&px)[OPS_PX]) {
+    uint32_t w[C];
+    if constexpr (C == 1) {
+        w[0] = px[0] | (px[1] << 8) | (px[2] << 16) | (px[3] << 24);
+    } else if constexpr (C == 3) {
+        w[0] = px[0] | (px[1] << 24);
+        w[1] = (px[1] >> 8) | (px[2] << 16);
+        w[2] = (px[2] >> 16) | (px[3] << 8);
+    } else {
+#pragma unroll
+        for (int k = 0; k < 4; ++k) w[k] = px[k];
+    }
+    if (n == OPS_PX && ((uintptr_t)d & 3) == 0) {
+        uint32_t* d4 = reinterpret_cast<uint32_t*>(d);
+#pragma unroll
+        for (int i = 0; i < C; ++i) d4[i] = w[i];
+    } else {
+        for (int i = 0; i < n * C; ++i) d[i] = (uint8_t)(w[i >> 2] >> (8 * (i & 3)));
+    }
+}
+
+// blockIdx.z: a run of MI images of the call (nimg in all); a lane's taps serve all of them
+template <int C, int MI>
+__global__ __launch_bounds__(OPS_THREADS) void k_remap_fixed_buf(Tab<const uint8_t> srcs, int nimg, int sh, int sw,
+                                                                 uint32_t sstep, uint32_t nbytes,
+                                                                 const int16_t* __restrict__ xy, size_t xy_step_e,
+                                                                 const uint16_t* __restrict__ fxy, size_t fxy_step_e,
+                                                                 int rows, int cols, Tab<uint8_t> dsts, size_t dstep) {
+    const Grp p = pixel_group(rows, cols);
+    if (p.n == 0) return;
+    const int n = p.n;
+    const int16_t* xr = xy + (size_t)p.y * xy_step_e + 2 * (size_t)p.x0;
+    const uint16_t* fr = fxy + (size_t)p.y * fxy_step_e + p.x0;
+    uint32_t mxy[OPS_PX], mf[OPS_PX];
+    if (n == OPS_PX && ((uintptr_t)xr & 15) == 0 && ((uintptr_t)fr & 7) == 0) {
+        const uint4 a = *reinterpret_cast<const uint4*>(xr);
+        const uint2 b = *reinterpret_cast<const uint2*>(fr);
+        mxy[0] = a.x; mxy[1] = a.y; mxy[2] = a.z; mxy[3] = a.w;
+        mf[0] = b.x; mf[1] = b.x >> 16; mf[2] = b.y; mf[3] = b.y >> 16;
+    } else {
+#pragma unroll
+        for (int k = 0; k < OPS_PX; ++k) {
+            const int kk = k < n ? k : n - 1;
+            mxy[k] = (uint32_t)(uint16_t)xr[2 * kk] | ((uint32_t)(uint16_t)xr[2 * kk + 1] << 16);
+            mf[k] = fr[kk];
+        }
+    }
+    RemapTap T[OPS_PX];
+    auto taps = [&](auto INc) {
+#pragma unroll
+        for (int k = 0; k < OPS_PX; ++k) {
+            const int f = (int)(mf[k] & 1023u);
+            T[k] = remap_tap<C, decltype(INc)::value>(sstep, sh, sw, (int)(int16_t)(mxy[k] & 0xffffu),
+                                                     (int)(int16_t)(mxy[k] >> 16), f & 31, f >> 5);
+        }
+    };
+    bool in = true;
+#pragma unroll
+    for (int k = 0; k < OPS_PX; ++k) {
+        const int sx = (int)(int16_t)(mxy[k] & 0xffffu), sy = (int)(int16_t)(mxy[k] >> 16);
+        in = in & (sx >= 0) & (sx <= sw - 2) & (sy >= 0) & (sy <= sh - 3);
+    }
+    if (__builtin_amdgcn_ballot_w64(!in) == 0) taps(std::true_type{});
+    else taps(std::false_type{});
+    const int i0 = (int)blockIdx.z * MI;
+    auto image = [&](int i) {
+        const RemapSrc S = remap_src(srcs.p[i], nbytes);
+        uint32_t px[OPS_PX];
+#pragma unroll
+        for (int k = 0; k < OPS_PX; ++k) px[k] = remap_apply<C>(S, T[k]);
+        store_packed<C>(dsts.p[i] + (size_t)p.y * dstep + (size_t)p.x0 * C, n, px);
+    };
+    if (i0 + MI <= nimg) {  // a whole run: no per-image guards between the images' loads
+#pragma unroll
+        for (int m = 0; m < MI; ++m) image(i0 + m);
+    } else {
+        for (int i = i0; i < nimg; ++i) image(i);
+    }
+}
+
+template <int C>
+__global__ __launch_bounds__(OPS_THREADS) void k_remap_float_buf(Tab<const uint8_t> srcs, int sh, int sw, uint32_t sstep,
+                                                                 uint32_t nbytes, const float* __restrict__ mapx,
+                                                                 const float* __restrict__ mapy, size_t map_step_f,
+                                                                 int rows, int cols, Tab<uint8_t> dsts, size_t dstep) {
+    const Grp p = pixel_group(rows, cols);
+    if (p.n == 0) return;
+    const RemapSrc S = remap_src(srcs.p[blockIdx.z], nbytes);
+    int sx[OPS_PX], sy[OPS_PX], fx[OPS_PX], fy[OPS_PX];
+    bool in = true;
+#pragma unroll
+    for (int k = 0; k < OPS_PX; ++k) {
+        const int x = min(p.x0 + k, cols - 1);
+        const int ix = round32(mapx[(size_t)p.y * map_step_f + x]);
+        const int iy = round32(mapy[(size_t)p.y * map_step_f + x]);
+        sx[k] = min(max(ix >> 5, -32768), 32767), sy[k] = min(max(iy >> 5, -32768), 32767);
+        fx[k] = ix & 31, fy[k] = iy & 31;
+        in = in & (sx[k] >= 0) & (sx[k] <= sw - 2) & (sy[k] >= 0) & (sy[k] <= sh - 3);
+    }
+    RemapTap T[OPS_PX];
+    auto taps = [&](auto INc) {
+#pragma unroll
+        for (int k = 0; k < OPS_PX; ++k)
+            T[k] = remap_tap<C, decltype(INc)::value>(sstep, sh, sw, sx[k], sy[k], fx[k], fy[k]);
+    };
+    if (__builtin_amdgcn_ballot_w64(!in) == 0) taps(std::true_type{});
+    else taps(std::false_type{});
+    uint32_t px[OPS_PX];
+#pragma unroll
+    for (int k = 0; k < OPS_PX; ++k) px[k] = remap_apply<C>(S, T[k]);
+    store_packed<C>(dsts.p[blockIdx.z] + (size_t)p.y * dstep + (size_t)p.x0 * C, p.n, px);
+}
+
+// the buffer form's limits: every source byte at a 31-bit offset, 24-bit row products
+static bool remap_buf_ok(int src_rows, int src_cols, size_t src_step, int C) {
+    const size_t bytes = (size_t)(src_rows - 1) * src_step + (size_t)src_cols * C;
+    return src_step < (1u << 23) && src_rows < (1 << 23) && bytes + 16 < 0x7fffffffu;
 }
 
 // ---- host side --------------------------------------------------------------------
@@ -946,50 +1004,36 @@ int tsm_remap_linear_fixed_batch_device(int n, const uint8_t* const* d_srcs, int
         xy_step < 4 * (size_t)cols || fxy_step < 2 * (size_t)cols || dst_step < (size_t)C * cols)
         return TSM_ERR_ARGUMENT;
     hipStream_t st = (hipStream_t)hip_stream;
-    // the LDS-tiled form when every source row starts on a dword (the usual case)
-    bool aligned = src_step % 4 == 0;
-    for (int i = 0; i < n && aligned; ++i) aligned = ((uintptr_t)d_srcs[i] & 3) == 0;
-    if (aligned && n > 0) {
-        // the tiles' source windows once for the call (stream-ordered scratch), then the tiles
-        const dim3 gt((cols + RT_COLS - 1) / RT_COLS, (rows + RT_ROWS - 1) / RT_ROWS, 1);
-        int4* boxes = nullptr;
-        hipError_t e = hipMallocAsync((void**)&boxes, (size_t)gt.x * gt.y * sizeof(int4), st);
-        if (e != hipSuccess) return status(e);
-        hipLaunchKernelGGL(k_remap_boxes, gt, dim3(OPS_THREADS), 0, st, d_xy, xy_step / 2, rows, cols, src_rows,
-                           src_cols, boxes);
-        for (int i = 0; i < n; i += kOpsBatch) {
-            const int k = min(kOpsBatch, n - i);
-            const dim3 g(gt.x, gt.y, k);
-            const Tab<const uint8_t> s = tab_of<const uint8_t>(d_srcs + i, k);
-            const Tab<uint8_t> d = tab_of<uint8_t>(d_dsts + i, k);
-#define TSM_REMAP_TILE(CC)                                                                               \
-            hipLaunchKernelGGL(k_remap_tile<CC>, g, dim3(OPS_THREADS), 0, st, s, src_rows, src_cols, src_step, \
-                               d_xy, xy_step / 2, d_fxy, fxy_step / 2, rows, cols, boxes, d, dst_step)
-            if (C == 1) TSM_REMAP_TILE(1);
-            else if (C == 3) TSM_REMAP_TILE(3);
-            else TSM_REMAP_TILE(4);
-#undef TSM_REMAP_TILE
-        }
-        e = hipGetLastError();
-        const hipError_t f = hipFreeAsync(boxes, st);
-        return status(e != hipSuccess ? e : f);
-    }
     // packed maps and output run as one row (the source is addressed through the maps)
     const bool dense = xy_step == 4 * (size_t)cols && fxy_step == 2 * (size_t)cols && dst_step == (size_t)C * cols &&
                        (long)rows * cols <= 0x7fffffffL;
     const int rr = dense ? 1 : rows, cc = dense ? rows * cols : cols;
+    const bool buf = remap_buf_ok(src_rows, src_cols, src_step, C);
+    // images a lane: their taps (offsets, weights, border handling) are computed once for the
+    // run (measured, 64 maps of 1242x375: 1 -> 72 us a call, 2 -> 58, 4 -> 53, 8 -> 53)
+    const int mi = n >= 4 ? 4 : (n >= 2 ? 2 : 1);
     for (int i = 0; i < n; i += kOpsBatch) {
         const int k = min(kOpsBatch, n - i);
         const dim3 g = row_blocks(rr, cc, k);
         const Tab<const uint8_t> s = tab_of<const uint8_t>(d_srcs + i, k);
         const Tab<uint8_t> d = tab_of<uint8_t>(d_dsts + i, k);
-#define TSM_REMAP_FIXED(CC)                                                                               \
-        hipLaunchKernelGGL(k_remap_fixed<CC>, g, dim3(OPS_THREADS), 0, st, s, src_rows, src_cols, src_step, \
-                           d_xy, xy_step / 2, d_fxy, fxy_step / 2, rr, cc, d, dst_step)
+        const uint32_t nb = (uint32_t)((size_t)(src_rows - 1) * src_step + (size_t)src_cols * C);
+#define TSM_REMAP_BUF(CC, M)                                                                                      \
+        hipLaunchKernelGGL((k_remap_fixed_buf<CC, M>), row_blocks(rr, cc, (k + M - 1) / M), dim3(OPS_THREADS), 0, st, \
+                           s, k, src_rows, src_cols, (uint32_t)src_step, nb, d_xy, xy_step / 2, d_fxy, fxy_step / 2,  \
+                           rr, cc, d, dst_step)
+#define TSM_REMAP_FIXED(CC)                                                                                       \
+        if (buf && mi == 4) TSM_REMAP_BUF(CC, 4);                                                                 \
+        else if (buf && mi == 2) TSM_REMAP_BUF(CC, 2);                                                            \
+        else if (buf) TSM_REMAP_BUF(CC, 1);                                                                       \
+        else                                                                                                      \
+            hipLaunchKernelGGL(k_remap_fixed<CC>, g, dim3(OPS_THREADS), 0, st, s, src_rows, src_cols, src_step,   \
+                               d_xy, xy_step / 2, d_fxy, fxy_step / 2, rr, cc, d, dst_step)
         if (C == 1) TSM_REMAP_FIXED(1);
         else if (C == 3) TSM_REMAP_FIXED(3);
         else TSM_REMAP_FIXED(4);
 #undef TSM_REMAP_FIXED
+#undef TSM_REMAP_BUF
     }
     return status(hipGetLastError());
 }
@@ -1007,9 +1051,15 @@ int tsm_remap_linear_float_device(const uint8_t* d_src, int src_rows, int src_co
     const dim3 g = row_blocks(rows, cols);
     const Tab<const uint8_t> s = tab_one<const uint8_t>(d_src);
     const Tab<uint8_t> d = tab_one<uint8_t>(d_dst);
-#define TSM_REMAP_FLOAT(CC)                                                                               \
-    hipLaunchKernelGGL(k_remap_float<CC>, g, dim3(OPS_THREADS), 0, st, s, src_rows, src_cols, src_step, \
-                       d_mapx, d_mapy, map_step / 4, rows, cols, d, dst_step)
+    const bool buf = remap_buf_ok(src_rows, src_cols, src_step, C);
+    const uint32_t nb = (uint32_t)((size_t)(src_rows - 1) * src_step + (size_t)src_cols * C);
+#define TSM_REMAP_FLOAT(CC)                                                                                     \
+    if (buf)                                                                                                    \
+        hipLaunchKernelGGL(k_remap_float_buf<CC>, g, dim3(OPS_THREADS), 0, st, s, src_rows, src_cols,           \
+                           (uint32_t)src_step, nb, d_mapx, d_mapy, map_step / 4, rows, cols, d, dst_step);      \
+    else                                                                                                        \
+        hipLaunchKernelGGL(k_remap_float<CC>, g, dim3(OPS_THREADS), 0, st, s, src_rows, src_cols, src_step,     \
+                           d_mapx, d_mapy, map_step / 4, rows, cols, d, dst_step)
     if (C == 1) TSM_REMAP_FLOAT(1);
     else if (C == 3) TSM_REMAP_FLOAT(3);
     else TSM_REMAP_FLOAT(4);

@@ -181,10 +181,10 @@ def test_remap_bit_exact(tsm, oracle, C, H, W):
 
 
 @pytest.mark.parametrize("C", [1, 3, 4])
-def test_remap_tile_paths(tsm, oracle, C):
-    """The LDS-tiled fixed-map kernel: tiles whose source window fits the LDS stage (smooth
-    warp), tiles that do not (scattered maps: the direct per-pixel path inside the tile),
-    both in one map, and a source at a 1-byte offset (the untiled kernel)."""
+def test_remap_wave_forms(tsm, oracle, C):
+    """The fixed-map kernel's two forms in one map: waves whose pixels' taps are all inside
+    the image (smooth warp: no clamps or weight selection) and waves with border or scattered
+    taps (rows 16..31 over and past the whole image), and a source at a 1-byte offset."""
     import torch
 
     rng = np.random.default_rng(31 + C)
@@ -202,6 +202,35 @@ def test_remap_tile_paths(tsm, oracle, C):
     assert mis.data_ptr() % 4 == 1
     got = tsm.remap(mis, torch.from_numpy(xy).cuda(), torch.from_numpy(fxy.view(np.int16)).cuda())
     assert np.array_equal(got.cpu().numpy(), want)
+
+
+@pytest.mark.parametrize("C", [1, 3, 4])
+@pytest.mark.parametrize("offset", [0, 1, 3])
+@pytest.mark.parametrize("sh,sw", [(9, 13), (1, 1), (2, 1), (1, 5)])
+def test_remap_last_row_end(tsm, oracle, C, offset, sh, sw):
+    """Taps at the very end of the source buffer: the window read of the last row's last
+    pixels runs past the image's bytes (those dwords read as 0 and carry weight 0); every
+    fraction, columns sw-3 .. sw, rows sh-3 .. sh, the source at a 0/1/3-byte offset."""
+    import torch
+
+    rng = np.random.default_rng(77 + C + offset + sh * sw)
+    src = rng.integers(1, 256, (sh, sw, C) if C > 1 else (sh, sw), dtype=np.uint8)
+    cols = np.arange(sw - 3, sw + 1)
+    rws = np.arange(sh - 3, sh + 1)
+    fr = np.arange(0, 1024, 37)
+    gx, gy, gf = np.meshgrid(cols, rws, fr, indexing="ij")
+    xy = np.stack([gx.ravel(), gy.ravel()], -1).astype(np.int16).reshape(1, -1, 2)
+    fxy = gf.ravel().astype(np.uint16).reshape(1, -1)
+    want = oracle.remap_linear_fixed(src, xy, fxy)
+    big = torch.empty(src.size + offset, dtype=torch.uint8, device="cuda")
+    dsrc = big[offset:].view(src.shape)
+    dsrc.copy_(torch.from_numpy(src).cuda())
+    got = tsm.remap(dsrc, torch.from_numpy(xy).cuda(), torch.from_numpy(fxy.view(np.int16)).cuda())
+    assert np.array_equal(got.cpu().numpy(), want)
+    # the float-map form over the same taps
+    mx = (gx.ravel() + (gf.ravel() & 31) / 32.0).astype(np.float32).reshape(1, -1)
+    my = (gy.ravel() + (gf.ravel() >> 5) / 32.0).astype(np.float32).reshape(1, -1)
+    assert np.array_equal(tsm.remap(src, mx, my), oracle.remap_linear_float(src, mx, my))
 
 
 def test_remap_float_map_edge_values(tsm, oracle):
