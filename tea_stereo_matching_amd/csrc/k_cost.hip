@@ -552,239 +552,6 @@ __global__ __launch_bounds__(CW_THREADS) __attribute__((amdgpu_waves_per_eu(E ==
 }
 
 // ---------------------------------------------------------------------------
-// cost-volume build, E = 3 RGB (193..196 labels: configs B, the demo pairs): the shift
-// register refilled from LDS
-// ---------------------------------------------------------------------------
-// The walk above moves the label axis one lane per step with 13 DPP shifts (one per record
-// word): 13 of its ~94 VALU a step.  Here a workgroup's 4 waves walk 4 consecutive
-// segments of one row of one view, and the whole range of varying records the 4 walks touch
-// (4 * SEG + 192 columns) is staged in LDS once, so the record entering a lane's slot at a
-// step is an LDS read (3 ds_read_b128 + 1 ds_read_b32 a lane, no VALU): lane l reads the
-// record 3 l columns from lane 0's, 144 B apart in the 48-B census array -- conflict-free
-// for ds_read_b128 (9 l mod 16 distinct) -- and 12 B apart in the colour array.  The fixed
-// records (one a step, wave-uniform) are staged beside them.  Same cells, same arithmetic,
-// same stores as the DPP walk.
-constexpr int CR_SEG = 48;                       // pixels a wave
-constexpr int CR_SPAN = 4 * CR_SEG;              // pixels a workgroup (4 waves)
-constexpr int CR_NV = CR_SPAN + 192;             // varying columns staged
-constexpr int CR_NF = CR_SPAN + 64;              // fixed columns staged (>= one read ahead)
-constexpr int CR_LDS = CR_NV * 52 + CR_NF * 52 + 4 * CR_SEG * 16;  // census + colour arrays, tails
-static_assert(CR_NV % 64 == 0 && CR_NF % 64 == 0, "stage fills run in whole 64-lane chunks");
-// with the tables' 4.5 KB, 40 KB a workgroup: four workgroups (16 waves) a CU
-static_assert(CR_LDS + (2 * CW_LUTB + 768) * 4 <= 40 * 1024, "four workgroups a CU");
-
-__host__ __device__ inline int cost_ring_units(int W) { return (W + CR_SPAN - 1) / CR_SPAN; }
-
-__global__ __launch_bounds__(CW_THREADS) __attribute__((amdgpu_waves_per_eu(4))) void k_cost_ring3(
-    const uint32_t* __restrict__ desc, const float* __restrict__ lutA, int lutA_n,
-    const float* __restrict__ lutB, float* __restrict__ vol, DevParams Pk, int nss) {
-    constexpr int E = 3, G = 6, NW = 13;
-    const DevParams P = Pk;
-    __shared__ __attribute__((aligned(16))) float s_lut[2 * CW_LUTB + 768];
-    extern __shared__ __attribute__((aligned(16))) u32x4 smem_stage[];
-    float* sB = s_lut;
-    float* sA = s_lut + 2 * CW_LUTB;
-    char* lds = reinterpret_cast<char*>(smem_stage);
-    u32x4* vcen = reinterpret_cast<u32x4*>(lds);                                  // [CR_NV][3]
-    uint32_t* vcol = reinterpret_cast<uint32_t*>(lds + CR_NV * 48);               // [CR_NV]
-    u32x4* fcen = reinterpret_cast<u32x4*>(lds + CR_NV * 52);                     // [CR_NF][3]
-    uint32_t* fcol = reinterpret_cast<uint32_t*>(lds + CR_NV * 52 + CR_NF * 48);  // [CR_NF]
-    f32x4* stT = reinterpret_cast<f32x4*>(lds + CR_NV * 52 + CR_NF * 52);          // [4][CR_SEG]
-    const int H = P.H, W = P.W, L = P.L, Lp = P.Lp;
-    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const int lane = threadIdx.x & 63;
-    pair_shift(blockIdx.z, P.pstride, desc, vol);
-    // XCD-aware unit order (see k_cost_walk): an XCD's blocks are neighbouring row spans
-    const int nb = gridDim.x, per = nb >> 3;
-    const int blk = (int)blockIdx.x < 8 * per ? ((int)blockIdx.x & 7) * per + ((int)blockIdx.x >> 3) : (int)blockIdx.x;
-    const bool active_blk = blk < 2 * H * nss;
-    const int u = active_blk ? blk : 0;
-    const int ss = u % nss, row = u / nss;
-    const int v = row & 1, y = row >> 1;  // views interleaved row by row (one XCD reads both)
-    const int x0 = ss * CR_SPAN;          // the workgroup's first pixel
-    const int foff = v == 0 ? -P.minD : P.minD;
-    const int xs0 = v == 0 ? x0 - 191 : x0;  // first staged varying column
-    const int hw = P.censusW >> 1, hh = P.censusH >> 1;
-    const bool rowOut = y - hh < 0 || y + hh >= H;
-    const uint32_t* dF = desc + ((size_t)v * H + y) * W * 16;
-    const uint32_t* dV = desc + ((size_t)(1 - v) * H + y) * W * 16;
-    auto clampx = [&](int x) { return x < 0 ? 0 : (x >= W ? W - 1 : x); };
-
-    // stage: census words as 3 x 16 B a column (lane i: column i / 3, quarter i % 3), colours
-    // as one word a column, by LDS-DMA; the 4 waves share the fills
-    // (every fill's extent is a whole number of 64-lane chunks, so no chunk writes past its
-    // array: CR_NV and CR_NF are multiples of 64)
-    for (int c = wave * 64; c < CR_NV * 3; c += 4 * 64) {
-        const int i = c + lane;
-        const int col = i / 3, q = i - col * 3;
-        __builtin_amdgcn_global_load_lds(reinterpret_cast<const u32x4*>(dV + (size_t)clampx(xs0 + col) * 16) + q,
-                                         vcen + c, 16, 0, 0);
-    }
-    for (int c = wave * 64; c < CR_NF * 3; c += 4 * 64) {
-        const int i = c + lane;
-        const int col = i / 3, q = i - col * 3;
-        __builtin_amdgcn_global_load_lds(reinterpret_cast<const u32x4*>(dF + (size_t)clampx(x0 + col + foff) * 16) + q,
-                                         fcen + c, 16, 0, 0);
-    }
-    for (int c = wave * 64; c < CR_NV; c += 4 * 64)
-        __builtin_amdgcn_global_load_lds(dV + (size_t)clampx(xs0 + c + lane) * 16 + 12, vcol + c, 4, 0, 0);
-    for (int c = wave * 64; c < CR_NF; c += 4 * 64)
-        __builtin_amdgcn_global_load_lds(dF + (size_t)clampx(x0 + c + lane + foff) * 16 + 12, fcol + c, 4, 0, 0);
-    for (int i = threadIdx.x; i < lutA_n; i += CW_THREADS) sA[i] = 2.f - lutA[i];
-    for (int i = threadIdx.x; i < 2 * CW_LUTB; i += CW_THREADS)
-        sB[i] = i < 188 ? lutB[i] : (i >= CW_LUTB ? -__int_as_float(0x7f800000) : 0.f);
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-    const int j0 = x0 + wave * CR_SEG;
-    const int count = min(CR_SEG, W - j0);
-    if (!active_blk || count <= 0) return;
-
-    const int fb = wave * CR_SEG;  // this wave's first fixed column in the stage
-    auto load_rec = [&](const u32x4* cen, const uint32_t* col, int i, uint32_t (&o)[NW]) {
-        const u32x4 a = cen[3 * i], b = cen[3 * i + 1], c = cen[3 * i + 2];
-        o[0] = a.x; o[1] = a.y; o[2] = a.z; o[3] = a.w;
-        o[4] = b.x; o[5] = b.y; o[6] = b.z; o[7] = b.w;
-        o[8] = c.x; o[9] = c.y; o[10] = c.z; o[11] = c.w;
-        o[12] = col[i];
-    };
-    float* orow = vol + ((size_t)v * H + y) * W * Lp + E * lane;
-
-    // the tail float4s (labels 192..195) of the wave's pixels, before the walk (k_cost_walk)
-    const bool tail = Lp > 64 * E;
-    if (tail) {
-        if (lane < count) {
-            const int j = j0 + lane;
-            const float inf = __int_as_float(0x7f800000);
-            uint32_t Fr[NW];
-            load_rec(fcen, fcol, fb + lane, Fr);
-            const int xf = j + foff;
-            const bool fixed_ok = !rowOut && xf - hw >= 0 && xf + hw < W;
-            const int klo = v == 0 ? j - (W - 1 - hw) : hw - j;
-            const int khi = v == 0 ? j - hw : W - 1 - hw - j;
-            float c4[4];
-#pragma unroll
-            for (int t = 0; t < 4; ++t) {
-                const int k = 64 * E + t;
-                c4[t] = inf;
-                if (k < L) {
-                    const u32x4* rv = reinterpret_cast<const u32x4*>(dV + (size_t)clampx(v == 0 ? j - k : j + k) * 16);
-                    const u32x4 qa = rv[0], qb = rv[1], qc = rv[2], qd = rv[3];
-                    const uint32_t Vr[NW] = {qa.x, qa.y, qa.z, qa.w, qb.x, qb.y, qb.z, qb.w, qc.x, qc.y, qc.z, qc.w, qd.x};
-                    uint32_t cen = 0;
-#pragma unroll
-                    for (int w = 0; w < 6; ++w) cen = bcnt_acc((Fr[w] & Vr[6 + w]) | (Fr[6 + w] & Vr[w]), cen);
-                    const int ai = (int)__builtin_amdgcn_sad_u8(Fr[NW - 1], Vr[NW - 1], 0u);
-                    const float cv = sA[ai] - sB[cen];
-                    c4[t] = (fixed_ok && k >= klo && k <= khi) ? cv : 2.f;
-                }
-            }
-            stT[fb + lane] = f32x4{c4[0], c4[1], c4[2], c4[3]};
-        }
-        __builtin_amdgcn_wave_barrier();
-    }
-
-    const int kmax = min(L, 64 * E) - 1;  // last real label of the lanes' 192
-    auto walk = [&](auto UPc, auto PADc) {
-    constexpr bool UP = decltype(UPc)::value == 0;
-    constexpr bool PAD = decltype(PADc)::value != 0;  // L < 192: labels L..191 are padding (+inf)
-    uint32_t padoff[E];  // census start: CW_LUTB for padding labels (sB there is -inf)
-#pragma unroll
-    for (int e = 0; e < E; ++e) padoff[e] = (PAD && E * lane + e >= L) ? CW_LUTB : 0u;
-    // warm-up: slot e of lane l holds label 3 l + e (rotation 0)
-    uint32_t V[NW][E];
-#pragma unroll
-    for (int e = 0; e < E; ++e) {
-        const int k = E * lane + e;
-        uint32_t r[NW];
-        load_rec(vcen, vcol, UP ? fb + 191 - k : fb + k, r);
-#pragma unroll
-        for (int w = 0; w < NW; ++w) V[w][e] = r[w];
-    }
-    // the column of the record entering lane l's slot at step t: UP, label 3 l at pixel
-    // j0 + t + 1 (column j0 + t + 1 - 3 l); DOWN, label 3 l + 2 (column j0 + t + 3 l + 3)
-    const int eb = UP ? fb + 192 - E * lane : fb + E * lane + E;
-    uint32_t FA[NW], FB[NW];
-    load_rec(fcen, fcol, fb, FA);
-    auto step = [&](auto Sc, bool fast, int t) {
-        constexpr int S = decltype(Sc)::value;
-        constexpr int R = S % E;
-        uint32_t(&F)[NW] = (S & 1) ? FB : FA;
-        uint32_t(&Fn)[NW] = (S & 1) ? FA : FB;
-        const int j = j0 + t;
-        load_rec(fcen, fcol, fb + t + 1, Fn);
-        uint32_t cen[E];
-#pragma unroll
-        for (int e = 0; e < E; ++e) cen[e] = padoff[e];
-#pragma unroll
-        for (int k = 0; k < 6; ++k)
-#pragma unroll
-            for (int e = 0; e < E; ++e) {
-                const int s = UP ? (e - R + E) % E : (e + R) % E;
-                cen[e] = bcnt_acc((F[k] & V[6 + k][s]) | (F[6 + k] & V[k][s]), cen[e]);
-            }
-        float c[E];
-#pragma unroll
-        for (int e = 0; e < E; ++e) {
-            const int s = UP ? (e - R + E) % E : (e + R) % E;
-            const int ai = (int)__builtin_amdgcn_sad_u8(F[NW - 1], V[NW - 1][s], 0u);
-            c[e] = sA[ai] - sB[cen[e]];
-        }
-        // the slot the census has just read for the last time takes the entering record
-        constexpr int s3 = UP ? (2 * E - 1 - R) % E : R % E;
-        {
-            uint32_t r[NW];
-            load_rec(vcen, vcol, eb + t, r);
-#pragma unroll
-            for (int w = 0; w < NW; ++w) V[w][s3] = r[w];
-        }
-        if (!fast) {
-            const int xf = j + foff;
-            const bool fixed_ok = !rowOut && xf - hw >= 0 && xf + hw < W;
-            const int klo = v == 0 ? j - (W - 1 - hw) : hw - j;
-            const int khi = v == 0 ? j - hw : W - 1 - hw - j;
-            if (!(fixed_ok && klo <= 0 && khi >= kmax)) {
-#pragma unroll
-                for (int e = 0; e < E; ++e) {
-                    const int k = E * lane + e;
-                    c[e] = (fixed_ok && k >= klo && k <= khi) || k >= L ? c[e] : 2.f;
-                }
-            }
-        }
-        if (fast || t < count) {
-            F3 o3;
-            o3.a = c[0];
-            o3.b = c[1];
-            o3.c = c[2];
-            *reinterpret_cast<F3*>(orow + (size_t)j * Lp) = o3;
-        }
-    };
-    const int jlo = max(v == 0 ? hw + kmax : hw, hw - foff);
-    const int jhi = min(v == 0 ? W - 1 - hw : W - 1 - hw - kmax, W - 1 - hw - foff);
-    const int tf_lo = jlo - j0;
-    const int tf_hi = min(jhi - j0, count - 1);
-    for (int t = 0; t < count; t += G) {
-        const bool fast = !rowOut && t >= tf_lo && t + G - 1 <= tf_hi;
-        [&]<int... Ss>(std::integer_sequence<int, Ss...>) {
-            (step(IC<Ss>{}, fast, t + Ss), ...);
-        }(std::make_integer_sequence<int, G>{});
-        if (tail) {
-            int ln;
-            asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0" : "=v"(ln));
-            if (ln < G && t + ln < count)
-                *reinterpret_cast<f32x4*>(vol + (((size_t)v * H + y) * W + j0 + t + ln) * Lp + 64 * E) = stT[fb + t + ln];
-        }
-    }
-    };
-    if (L >= 64 * E) {
-        if (v == 0) walk(IC<0>{}, IC<0>{});
-        else walk(IC<1>{}, IC<0>{});
-    } else {
-        if (v == 0) walk(IC<0>{}, IC<1>{});
-        else walk(IC<1>{}, IC<1>{});
-    }
-}
-
-// ---------------------------------------------------------------------------
 // launchers
 // ---------------------------------------------------------------------------
 void launch_pack(const PairIn& in, size_t step, uint32_t* img, const DevParams& P, hipStream_t st) {
@@ -868,15 +635,8 @@ int launch_cost_volume(const uint32_t* desc, const float* lutA, int lutA_n, cons
         else launch_cost_t<E, false, false>(desc, lutA, lutA_n, lutB, vol, P, st);                 \
     }
     switch (cost_lanes(P)) {  // E = 3 and 5 are never asked for in mask mode
-        case 3: if (hsi) {
-                    launch_cost_t<3, true, false>(desc, lutA, lutA_n, lutB, vol, P, st);
-                } else {
-                    const int nss = cost_ring_units(P.W);
-                    const dim3 g((2 * P.H * nss + 7) / 8 * 8, 1, P.npairs);
-                    ensure_lds_limit((const void*)k_cost_ring3, CR_LDS);
-                    hipLaunchKernelGGL(k_cost_ring3, g, dim3(CW_THREADS), CR_LDS, st, desc, lutA, lutA_n, lutB, vol, P, nss);
-                    trace_point("k_cost_ring3", st);
-                }
+        case 3: if (hsi) launch_cost_t<3, true, false>(desc, lutA, lutA_n, lutB, vol, P, st);
+                else launch_cost_t<3, false, false>(desc, lutA, lutA_n, lutB, vol, P, st);
                 break;
         case 4: CASE(4) break;
         case 5: if (hsi) launch_cost_t<5, true, false>(desc, lutA, lutA_n, lutB, vol, P, st);
