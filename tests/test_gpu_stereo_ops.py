@@ -233,6 +233,39 @@ def test_remap_last_row_end(tsm, oracle, C, offset, sh, sw):
     assert np.array_equal(tsm.remap(src, mx, my), oracle.remap_linear_float(src, mx, my))
 
 
+def test_remap_wide_step_fallback(tsm, oracle):
+    """A source whose row step is past the buffer form's 2^23-byte limit runs the 64-bit
+    gather kernels (k_remap_fixed / k_remap_float): same outputs, borders included."""
+    from tea_stereo_matching_amd import _native as N
+
+    lib = N.load()
+    hip = _Hip()
+    try:
+        rng = np.random.default_rng(12)
+        sh, sw, C = 3, 40, 3
+        step = (1 << 23) + 64
+        src = rng.integers(0, 256, (sh, sw, C), dtype=np.uint8)
+        wide = np.zeros((sh, step), np.uint8)
+        wide[:, :sw * C] = src.reshape(sh, -1)
+        H, W = 6, 50
+        _, _, xy, fxy = _maps(rng, H, W, sh, sw)
+        xy[0, :8, 0] = [-2, -1, 0, sw - 2, sw - 1, sw, 5, 7]
+        xy[0, :8, 1] = [0, 1, -1, sh - 1, sh - 2, 1, sh, -2]
+        mx = rng.uniform(-2, sw + 1, (H, W)).astype(np.float32)
+        my = rng.uniform(-2, sh + 1, (H, W)).astype(np.float32)
+        ds = hip.put(wide)
+        dxy, dfxy, dmx, dmy = hip.put(xy), hip.put(fxy), hip.put(mx), hip.put(my)
+        out = np.zeros((H, W, C), np.uint8)
+        do = hip.put(out)
+        assert lib.tsm_remap_linear_fixed_device(ds, sh, sw, step, C, dxy, 4 * W, dfxy, 2 * W, H, W, do, C * W,
+                                                 None) == 0
+        assert np.array_equal(hip.get(do, out), oracle.remap_linear_fixed(src, xy, fxy))
+        assert lib.tsm_remap_linear_float_device(ds, sh, sw, step, C, dmx, dmy, 4 * W, H, W, do, C * W, None) == 0
+        assert np.array_equal(hip.get(do, out), oracle.remap_linear_float(src, mx, my))
+    finally:
+        hip.free()
+
+
 def test_remap_float_map_edge_values(tsm, oracle):
     rng = np.random.default_rng(4)
     src = rng.integers(0, 256, (30, 40, 3), dtype=np.uint8)
