@@ -191,7 +191,7 @@ def test_remap_wave_forms(tsm, oracle, C):
     H, W, sh, sw = 70, 300, 64, 290
     src = rng.integers(0, 256, (sh, sw, C) if C > 1 else (sh, sw), dtype=np.uint8)
     _, _, xy, fxy = _maps(rng, H, W, sh, sw)
-    # rows 16..31 scattered over (and past) the whole image: no tile window fits
+    # rows 16..31 scattered over (and past) the whole image: border waves
     xy[16:32, :, 0] = rng.integers(-10, sw + 10, (16, W))
     xy[16:32, :, 1] = rng.integers(-10, sh + 10, (16, W))
     want = oracle.remap_linear_fixed(src, xy, fxy)
