@@ -51,6 +51,145 @@ enum class ColorModel { RGB = 0, HSI = 1 };
 /** stereo_utils.h:200-204 */
 enum class CensusWin { CENSUSWIN_9x7 = 0, CENSUSWIN_7x5 = 1 };
 
+/** stereo_utils.h:206-244, defaults stereo_utils.cpp:271-326: the (Selective)
+ *  AD-Census(-HSI) parameter set, member for member.  The reference keeps one inside
+ *  ADCensus (ADCensus.cpp:278), set from the colour model by setMatchingStrategy; here
+ *  ADCensus::getParams / setParams also exchange it (extensions). */
+class ADCensusParams {
+public:
+    ADCensusParams() { setADCensusParams(ColorModel::RGB); }
+    ADCensusParams(const ColorModel& colorModel) { setADCensusParams(colorModel); }
+    ~ADCensusParams() {}
+
+    void setADCensusParams(const ColorModel& colorModel) {
+        lambdaAD = 10.f;
+        censusWin = CensusWin::CENSUSWIN_9x7;
+        lambdaCensus = 30.f;
+        lambdaHue = 1.f;
+        lambdaSaturation = 2.5f;
+        lambdaIntensity = 2.5f;
+        iterations = 4;
+        pi1 = 1.f;
+        pi2 = 3.f;
+        dispTolerance = 0;
+        votingThresh = 20;
+        votingRatioThresh = 0.4f;
+        maxSearchDepth = 20;
+        blurKernelSize = 3;
+        cannyThresh1 = 30;
+        cannyThresh2 = 90;
+        cannyKernelSize = 3;
+        if (colorModel == ColorModel::RGB) {
+            colorThresh1 = 20;
+            colorThresh2 = 6;
+            maxLength1 = 34;
+            maxLength2 = 17;
+            colorDiff = 15;
+            saturationThresh1 = saturationThresh2 = 0;  // the reference assigns NULL
+            intensityThresh1 = intensityThresh2 = 0;
+        } else {  // HSI (and the reference's default branch)
+            colorThresh1 = 5;
+            colorThresh2 = 1;
+            maxLength1 = 17;
+            maxLength2 = 8;
+            colorDiff = 3;
+            saturationThresh1 = 10;
+            saturationThresh2 = 2;
+            intensityThresh1 = 12;
+            intensityThresh2 = 3;
+        }
+    }
+
+    float lambdaAD;
+    CensusWin censusWin;
+    float lambdaCensus;
+    float lambdaHue;
+    float lambdaSaturation;
+    float lambdaIntensity;
+    int colorThresh1;
+    int colorThresh2;
+    int saturationThresh1;
+    int saturationThresh2;
+    int intensityThresh1;
+    int intensityThresh2;
+    int maxLength1;
+    int maxLength2;
+    int iterations;
+    int colorDiff;
+    float pi1;
+    float pi2;
+    int dispTolerance;
+    int votingThresh;
+    float votingRatioThresh;
+    int maxSearchDepth;
+    int blurKernelSize;
+    int cannyThresh1;
+    int cannyThresh2;
+    int cannyKernelSize;
+
+    /** The C ABI's form (include/tsm_adcensus.h tsm_adc_params), and back. */
+    tsm_adc_params toC() const {
+        tsm_adc_params c{};
+        c.lambda_ad = lambdaAD;
+        c.census_win = (int)censusWin;
+        c.lambda_census = lambdaCensus;
+        c.lambda_hue = lambdaHue;
+        c.lambda_saturation = lambdaSaturation;
+        c.lambda_intensity = lambdaIntensity;
+        c.color_thresh1 = colorThresh1;
+        c.color_thresh2 = colorThresh2;
+        c.saturation_thresh1 = saturationThresh1;
+        c.saturation_thresh2 = saturationThresh2;
+        c.intensity_thresh1 = intensityThresh1;
+        c.intensity_thresh2 = intensityThresh2;
+        c.max_length1 = maxLength1;
+        c.max_length2 = maxLength2;
+        c.iterations = iterations;
+        c.color_diff = colorDiff;
+        c.pi1 = pi1;
+        c.pi2 = pi2;
+        c.disp_tolerance = dispTolerance;
+        c.voting_thresh = votingThresh;
+        c.voting_ratio_thresh = votingRatioThresh;
+        c.max_search_depth = maxSearchDepth;
+        c.blur_kernel_size = blurKernelSize;
+        c.canny_thresh1 = cannyThresh1;
+        c.canny_thresh2 = cannyThresh2;
+        c.canny_kernel_size = cannyKernelSize;
+        return c;
+    }
+    static ADCensusParams fromC(const tsm_adc_params& c) {
+        ADCensusParams p;
+        p.lambdaAD = c.lambda_ad;
+        p.censusWin = (CensusWin)c.census_win;
+        p.lambdaCensus = c.lambda_census;
+        p.lambdaHue = c.lambda_hue;
+        p.lambdaSaturation = c.lambda_saturation;
+        p.lambdaIntensity = c.lambda_intensity;
+        p.colorThresh1 = c.color_thresh1;
+        p.colorThresh2 = c.color_thresh2;
+        p.saturationThresh1 = c.saturation_thresh1;
+        p.saturationThresh2 = c.saturation_thresh2;
+        p.intensityThresh1 = c.intensity_thresh1;
+        p.intensityThresh2 = c.intensity_thresh2;
+        p.maxLength1 = c.max_length1;
+        p.maxLength2 = c.max_length2;
+        p.iterations = c.iterations;
+        p.colorDiff = c.color_diff;
+        p.pi1 = c.pi1;
+        p.pi2 = c.pi2;
+        p.dispTolerance = c.disp_tolerance;
+        p.votingThresh = c.voting_thresh;
+        p.votingRatioThresh = c.voting_ratio_thresh;
+        p.maxSearchDepth = c.max_search_depth;
+        p.blurKernelSize = c.blur_kernel_size;
+        p.cannyThresh1 = c.canny_thresh1;
+        p.cannyThresh2 = c.canny_thresh2;
+        p.cannyKernelSize = c.canny_kernel_size;
+        return p;
+    }
+};
+
 /** Non-owning BGR u8 image (the fields of a CV_8UC3 cv::Mat the matcher uses). */
 struct ImageView {
     const std::uint8_t* data = nullptr;
@@ -190,6 +329,17 @@ public:
         disparities = std::move(out);
     }
 
+    /** Extension: the active parameter set (the reference's m_paMatching). */
+    ADCensusParams getParams() const {
+        tsm_adc_params c{};
+        check(tsm_adc_get_params(h_, &c));
+        return ADCensusParams::fromC(c);
+    }
+    /** Extension: replace the parameter set (setMatchingStrategy resets it to the model's). */
+    void setParams(const ADCensusParams& params) {
+        const tsm_adc_params c = params.toC();
+        check(tsm_adc_set_params(h_, &c));
+    }
     /** Extension: reproduce the reference's racy omp-static scanline on T threads. */
     void setOmpEmulation(int threads) { check(tsm_adc_set_omp_emulation(h_, threads)); }
     /** Extension: number of concurrent pair pipelines for the batch form. */

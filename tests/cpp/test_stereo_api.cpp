@@ -1,6 +1,7 @@
 // C++ API check (run by tests/test_gpu_cpp_api.py on the GPU box): the reference's
 // usage pattern (README.md:177-191) against stereo::ADCensus from include/stereo.h,
 // including the reference's exception types and messages.
+#include <cstring>
 #include <cstdio>
 #include <cstdlib>
 #include <string>
@@ -45,7 +46,23 @@ int main(int argc, char** argv) {
             for (int c = 0; c < 3; ++c) r[(y * W + x) * 3 + c] = l[(y * W + std::min(W - 1, x + 6)) * 3 + c];
 
     stereo::ADCensus adcensus;
+    // the parameter set: the engine's per-model defaults are the reference's
+    // (stereo_utils.cpp:271-326; a new matcher is in the HSI model, ADCensus.cpp:409-420)
+    auto same = [](const stereo::ADCensusParams& a, const stereo::ADCensusParams& b) {
+        const tsm_adc_params x = a.toC(), y = b.toC();
+        return std::memcmp(&x, &y, sizeof x) == 0;
+    };
+    CHECK(same(adcensus.getParams(), stereo::ADCensusParams(stereo::ColorModel::HSI)));
     adcensus.setMatchingStrategy(stereo::ColorModel::RGB, false, false);
+    CHECK(same(adcensus.getParams(), stereo::ADCensusParams(stereo::ColorModel::RGB)));
+    {
+        stereo::ADCensusParams p(stereo::ColorModel::RGB);
+        p.maxLength1 = 30;
+        p.votingRatioThresh = 0.5f;
+        adcensus.setParams(p);
+        CHECK(same(adcensus.getParams(), p));
+        adcensus.setParams(stereo::ADCensusParams(stereo::ColorModel::RGB));
+    }
     adcensus.setMinMaxDisparity(0, 16);
     stereo::ImageView L{l.data(), H, W, (size_t)W * 3}, R{r.data(), H, W, (size_t)W * 3};
     stereo::DisparityMap d;

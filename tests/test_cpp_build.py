@@ -48,3 +48,19 @@ def test_mixed_opencv_modes_fail_to_link(tmp_path):
     assert "stereo::light_v1::ADCensus" in nm and "stereo::cvmat_v1::ADCensus" in nm
     r = subprocess.run(["g++", objs[0], objs[1], "-o", str(tmp_path / "mixed")], capture_output=True, text=True)
     assert r.returncode != 0 and "undefined reference" in r.stderr, r.stderr
+
+
+@pytest.mark.skipif(shutil.which("g++") is None, reason="no g++")
+def test_adcensus_params_defaults_match_reference(tmp_path):
+    """include/stereo.h's ADCensusParams (reference stereo_utils.h:206-244) carries the
+    reference's per-model defaults (stereo_utils.cpp:271-326) and converts to the C ABI's
+    tsm_adc_params and back; header-only, so it runs without the library or a GPU."""
+    import subprocess
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    exe = str(tmp_path / "params")
+    subprocess.run(["g++", "-std=c++20", "-Wall", "-Werror", "-I", os.path.join(root, "include"),
+                    os.path.join(root, "tests", "cpp", "test_params.cpp"), "-o", exe], check=True)
+    r = subprocess.run([exe], capture_output=True, text=True)
+    assert r.returncode == 0, r.stderr
+    assert "params ok" in r.stdout
