@@ -44,6 +44,8 @@ $(LIB): $(OBJS)
 #   make exp X=name PATCH=tools/probes/name.patch [DEFS=...]
 EXP = build/exp/$(X)
 exp:
+	@test -n "$(X)" || { echo 'make exp: X=<name> required'; exit 1; }
+	@test -z "$(PATCH)" || test -f "$(PATCH)" || { echo 'make exp: PATCH=$(PATCH) not found'; exit 1; }
 	rm -rf $(EXP)/tea_stereo_matching_amd $(EXP)/include $(EXP)/obj
 	mkdir -p $(EXP)/tea_stereo_matching_amd $(EXP)/obj
 	cp -r include $(EXP)/include

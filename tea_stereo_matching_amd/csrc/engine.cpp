@@ -42,14 +42,16 @@ static bool trace_enabled() {
     return trace;
 }
 
-uint32_t* trace_flag() {
+// one flag per (device, stream): concurrent pipelines never report or clear each other's
+// violations; read and cleared in stream order on the stream being traced
+uint32_t* trace_flag(hipStream_t st) {
     if (!trace_enabled()) return nullptr;
     static std::mutex mu;
-    static std::map<int, uint32_t*> per_dev;
+    static std::map<std::pair<int, hipStream_t>, uint32_t*> per_stream;
     int dev = 0;
     (void)hipGetDevice(&dev);
     std::lock_guard<std::mutex> g(mu);
-    uint32_t*& f = per_dev[dev];
+    uint32_t*& f = per_stream[{dev, st}];
     if (!f && hipMalloc((void**)&f, 64) == hipSuccess) (void)hipMemset(f, 0, 64);
     return f;
 }
@@ -59,11 +61,13 @@ void trace_point(const char* what, hipStream_t st) {
     hipError_t le = hipGetLastError();
     hipError_t se = hipStreamSynchronize(st);
     std::fprintf(stderr, "[tsm] %-40s launch=%s sync=%s\n", what, hipGetErrorString(le), hipGetErrorString(se));
-    if (uint32_t* f = trace_flag()) {
+    if (uint32_t* f = trace_flag(st)) {
         uint32_t v[2] = {0, 0};
-        if (hipMemcpy(v, f, 8, hipMemcpyDeviceToHost) == hipSuccess && v[0] != 0) {
+        if (hipMemcpyAsync(v, f, 8, hipMemcpyDeviceToHost, st) == hipSuccess && hipStreamSynchronize(st) == hipSuccess &&
+            v[0] != 0) {
             std::fprintf(stderr, "[tsm] %-40s PROTOCOL CHECK FAILED: kind=%u detail=0x%08x\n", what, v[0], v[1]);
-            (void)hipMemset(f, 0, 8);
+            (void)hipMemsetAsync(f, 0, 8, st);
+            (void)hipStreamSynchronize(st);
         }
     }
     std::fflush(stderr);

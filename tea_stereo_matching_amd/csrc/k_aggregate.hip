@@ -232,7 +232,7 @@ struct AggStream {
     int cpl;               // chunks per line
     int nlv;               // lines per view
     int nl;                // lines of both views
-    uint32_t* err;         // CHK: the trace flag (trace_flag())
+    uint32_t* err;         // CHK: the stream's trace flag (trace_flag(st))
     int slices_x;          // > 1: the label slices interleaved along blockIdx.x (see k_agg_split)
 };
 
@@ -616,9 +616,9 @@ constexpr size_t kLdsBytes = 160 * 1024;
 
 template <bool FUSED, int QT, bool BIG>
 static void launch_split_t(const AggStream& S, const DevParams& P, dim3 grid, size_t lds, hipStream_t st) {
-    if (S.err) {  // TSM_TRACE: the descriptor-checked variant (generic label count)
-        ensure_lds_limit((const void*)k_agg_split<FUSED, 0, BIG, true>, kLdsBytes);
-        hipLaunchKernelGGL((k_agg_split<FUSED, 0, BIG, true>), grid, dim3(AX_THREADS), lds, st, S, P);
+    if (S.err) {  // TSM_TRACE: the descriptor-checked variant of the instance production runs
+        ensure_lds_limit((const void*)k_agg_split<FUSED, QT, BIG, true>, kLdsBytes);
+        hipLaunchKernelGGL((k_agg_split<FUSED, QT, BIG, true>), grid, dim3(AX_THREADS), lds, st, S, P);
         return;
     }
     ensure_lds_limit((const void*)k_agg_split<FUSED, QT, BIG>, kLdsBytes);
@@ -667,7 +667,7 @@ int launch_aggregation_pass(float* vol, const uint32_t* arms, const int32_t* ws,
     S.cpl = (S.n + AS_SEG - 1) / AS_SEG;
     S.nlv = horizontal ? P.H : P.W;
     S.nl = 2 * S.nlv;
-    S.err = trace_flag();
+    S.err = trace_flag(st);
     const int ncu = P.ncu;
     const int G = S.nl < ncu ? S.nl : ncu;
     // every pass through the role-split streamer (round 4, same box: 409 against 406.5

@@ -424,7 +424,8 @@ __global__ __launch_bounds__(VD_WAVES * 64) void k_vote_decide_wave(
             if (lane == 0) long_list[atomicAdd(&counts[2], 1)] = k;
             continue;
         }
-        for (int d = lane; d < L; d += 64) h[d] = 0;  // a wave's LDS operations stay in order
+        for (int d = lane; d < L; d += 64) h[d] = 0;
+        wave_lds_sync();  // the zeroed bins before any lane's atomics (lanes share the histogram)
         const int p = out_list[r];
         const int v = cvote[r];
         const int y = p / W, x = p - y * W;
@@ -483,6 +484,7 @@ __global__ __launch_bounds__(VD_WAVES * 64) void k_vote_decide_wave(
                 }
             }
         }
+        wave_lds_sync();  // every lane's atomics before the argmax reads
         uint64_t best = ~0ull;
         for (int d = lane; d < L; d += 64) {
             const uint64_t key = ((uint64_t)(0xffffffffu - (uint32_t)h[d]) << 32) | (uint32_t)d;

@@ -473,6 +473,14 @@ __global__ void k_remap_float(Tab<const uint8_t> srcs, int sh, int sw, size_t ss
 //    2-term dot product with the horizontal weights.  Exact: sum_ij t_ij w_ij * 32 + 2^14
 //    >> 15 with w = (32-fx | fx) x (32-fy | fy) equals ((32-fx) v0 + fx v1 + 512) >> 10,
 //    and with the horizontal weights scaled by 64 the result is byte 2 of the dot product.
+//  * the last row's last windows read 12 B of which the tail dwords lie past num_records: the
+//    form relies on the raw buffer range check being per dword (in-range dwords return their
+//    data, the others 0), which gfx950 does (tests/test_gpu_stereo_ops.py
+//    test_remap_last_row_end pins it on the box).  The library is built for gfx950 only; the
+//    guard below stops a device compile for any target where that was not measured.
+#if defined(__HIP_DEVICE_COMPILE__) && !defined(__gfx950__)
+#error "k_remap_*_buf: per-dword buffer range checks are verified on gfx950 only"
+#endif
 typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
 typedef uint32_t u32x3v __attribute__((ext_vector_type(3)));
 

@@ -216,4 +216,13 @@ __device__ __forceinline__ int wave_sum_i(int v) {
 
 __device__ __forceinline__ int lane_id() { return threadIdx.x & 63; }
 
+// Orders one wave's LDS accesses across its lanes (lanes sharing LDS words without a workgroup
+// barrier): every access before it completes before any after it, and the compiler moves none
+// across it.
+__device__ __forceinline__ void wave_lds_sync() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
 }  // namespace tsm

@@ -11,10 +11,10 @@ namespace tsm {
 // Debug hook (engine.cpp): with TSM_TRACE=1 in the environment, synchronise the stream
 // after every launch and log the kernel name + status to stderr.  No-op otherwise.
 void trace_point(const char* what, hipStream_t st);
-// With TSM_TRACE=1: a zeroed two-word device flag of the current device that checked kernel
+// With TSM_TRACE=1: a zeroed two-word device flag of the current device and stream `st` that checked kernel
 // variants set on a protocol violation ([0] = kind, [1] = detail) instead of addressing
 // outside their buffers; trace_point reports and clears it.  nullptr when tracing is off.
-uint32_t* trace_flag();
+uint32_t* trace_flag(hipStream_t st);
 
 // Raise `kernel`'s dynamic-LDS limit to `bytes` on the current device, once per (kernel,
 // device) and thread-safe (engine.cpp): handles on several threads may launch at once, and

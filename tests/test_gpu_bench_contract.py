@@ -38,3 +38,9 @@ def test_bench_json_line_small_batch():
     assert r["algorithmic_bytes_per_launch"] == 4 * 193 * 1242 * 375 * 2 + 2 * 3 * 1242 * 375
     assert d["verified"] is True, d.get("verification")
     assert d["library"].endswith("libtsm_adcensus.so")
+    # the headline loop runs without stage events; the repeats and the compact summary
+    # (the driver keeps the line's tail) come last
+    t = d["timed_region"]
+    assert t["stage_events"] is False and len(t["step_ms_min_median_max"]) == 3
+    assert t["repeat_with_stage_events"]["pairs_per_s"] > 0 and t["repeat_without"]["pairs_per_s"] > 0
+    assert list(d)[-1] == "summary"
