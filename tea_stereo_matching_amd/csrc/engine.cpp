@@ -436,10 +436,25 @@ DevParams make_params(const tsm_adc* h, int H, int W) {
     return P;
 }
 
+// A group stream on a hardware queue of its own.  Plain streams share the process's
+// GPU_MAX_HW_QUEUES hardware queues (4 by default), and once those are taken a new stream
+// joins an existing queue: measured on the box, a handle created while another handle
+// held its two streams got both of its group streams on ONE queue, so its two groups ran
+// one after the other (385 against 420 pairs/s on the bench batch, tools/headline_ab.py,
+// profiles/r06_stream_queues.txt).  A stream created with a CU mask always gets a new
+// queue; the mask names every CU, so nothing else changes.
+hipError_t create_group_stream(const tsm_adc* h, hipStream_t* s) {
+    std::vector<uint32_t> mask((size_t)(h->ncu + 31) / 32, 0xffffffffu);
+    if (h->ncu % 32) mask.back() = (1u << (h->ncu % 32)) - 1u;
+    if (hipExtStreamCreateWithCUMask(s, (uint32_t)mask.size(), mask.data()) == hipSuccess) return hipSuccess;
+    (void)hipGetLastError();
+    return hipStreamCreateWithFlags(s, hipStreamNonBlocking);
+}
+
 // Workspace for groups of up to K pairs of H x W at the current range and model.
 int ensure_workspace(tsm_adc* h, Workspace* w, int H, int W, int K) {
     const int L = h->max_disparity - h->min_disparity + 1;
-    if (w->stream == nullptr) HIP_OK(hipStreamCreateWithFlags(&w->stream, hipStreamNonBlocking));
+    if (w->stream == nullptr) HIP_OK(create_group_stream(h, &w->stream));
     const tsm_adc_params& p = h->params;
     if (w->H == H && w->W == W && w->L == L && w->maxD == h->max_disparity && w->model == h->color_model &&
         w->lambda_ad == p.lambda_ad && w->lambda_census == p.lambda_census && w->cap >= K)

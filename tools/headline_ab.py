@@ -52,10 +52,11 @@ def main():
             ts.append(time.perf_counter() - t0)
         return n * k / sum(ts), min(ts) * 1e3, max(ts) * 1e3
 
-    long_m = handle()
+    long_m = None  # created at its first use
     for r in range(a.reps):
         for v in a.variants.split(","):
             if v == "long":
+                long_m = long_m or handle()
                 m = long_m
             else:
                 m = handle(20 if v == "omp20" else 0)
