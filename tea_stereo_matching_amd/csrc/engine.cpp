@@ -330,7 +330,7 @@ void layout_slot(Workspace* w, SlotLayout& S, int H, int W, int L, int model) {
     S.take(B.out_list, N * 4);
     S.take(B.cvote, N * 4);
     S.take(B.csamp, N * 20 * 2);
-    S.take(B.bsum, 2 * refine_scan_blocks((int)N) * 4 + 64);
+    S.take(B.flags, refine_flag_words(H, W) * 8 + 64);
     S.take(B.hv_list, N * 4);
     S.take(B.long_list, N * 4);
     S.take(B.counts, 16);

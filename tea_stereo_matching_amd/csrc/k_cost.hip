@@ -499,10 +499,18 @@ __global__ __launch_bounds__(CW_THREADS) __attribute__((amdgpu_waves_per_eu(E ==
                 o5.e = c[4];
                 *reinterpret_cast<F5*>(orow + (size_t)j * Lp) = o5;
             }
+            // E = 4 / 8: 16-B pieces, plain stores like E = 3 / 5.  A pixel vector of 260 labels is
+            // 1040 B, not a whole number of 64-B granules: its neighbours' stores complete the
+            // shared granules in L2 only if they stay there -- as non-temporal stores config C
+            // wrote 3.46 GB for a 3.09 GB volume and the walk took 0.98 ms; plain: 3.12 GB,
+            // 0.83 ms (round 6, profiles/r06_cost_walk_C.txt)
+            if constexpr (E == 4 || E == 8) {  // (E = 5 is the F5 store above, whole)
 #pragma unroll
-            for (int q = 0; q < E / 4; ++q)
-                if (kb + E * lane + 4 * q < Lp)
-                    st_stream(orow + (size_t)j * Lp + 4 * q, f32x4{c[4 * q], c[4 * q + 1], c[4 * q + 2], c[4 * q + 3]});
+                for (int q = 0; q < E / 4; ++q)
+                    if (kb + E * lane + 4 * q < Lp)
+                        *reinterpret_cast<f32x4*>(orow + (size_t)j * Lp + 4 * q) =
+                            f32x4{c[4 * q], c[4 * q + 1], c[4 * q + 2], c[4 * q + 3]};
+            }
         }
         // advance: view 0: the slot of offset E-1 becomes offset 0 of the next rotation,
         // fed from lane-1 (lane 0 has no source and keeps `old`, the entering word);

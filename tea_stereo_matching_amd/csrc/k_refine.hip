@@ -70,8 +70,7 @@ __device__ __forceinline__ void region_arms(uint32_t a, bool hf, int& oA, int& o
     else { oA = lf; oB = rt; iA = up; iB = dn; }
 }
 
-// Raster-order ranks of the outliers per block of SC_BLOCK pixels (k_oscan_count, then
-// k_oscan_scatter with the preceding blocks' counts).
+// Raster-order ranks of the outliers per block of SC_BLOCK pixels (k_vote_prep).
 constexpr int SC_THREADS = 256, SC_ITEMS = 16, SC_BLOCK = SC_THREADS * SC_ITEMS;
 
 // the SC_ITEMS disparities of a thread (16-B loads when the run is whole; the buffers are
@@ -123,57 +122,110 @@ constexpr int RW_B = 8;          // region walks: row-segment pixels loaded a ro
 // high-vote outlier, its region and then the low-vote outliers ranked just before it back
 // to the previous high-vote one: exactly the histogram the reference carries in raster
 // order (:1132-1151).  No per-pixel vote / sample / flag maps and no second scan.
-__global__ void k_oscan_count(const int32_t* __restrict__ disp, int n, int minD, int32_t* __restrict__ bsum,
-                              size_t ps) {
-    pair_shift(blockIdx.z, ps, disp, bsum);
-    __shared__ int sa[SC_THREADS], sb[SC_THREADS];
-    const int base = blockIdx.x * SC_BLOCK + threadIdx.x * SC_ITEMS;
-    int dv[SC_ITEMS];
-    load_items(disp, base, n, dv);
-    int a = 0, b = 0;
-#pragma unroll
-    for (int k = 0; k < SC_ITEMS; ++k) a += dv[k] < minD ? 1 : 0;
-    block_scan2(a, b, sa, sb);
-    if (threadIdx.x == SC_THREADS - 1) {
-        bsum[2 * blockIdx.x] = sa[SC_THREADS - 1];
-        bsum[2 * blockIdx.x + 1] = 0;
-    }
+//
+// Single-pass scans: a block publishes its count (tagged with the launch's epoch, so a
+// stale value from an earlier launch never matches), then sums its predecessors' counts,
+// waiting for each to appear.  Workgroups are dispatched in index order, so every block
+// waited on is resident or finished and itself waits only on earlier ones: no deadlock.
+// One launch instead of a count launch and a scatter launch (round 6: 10 fewer launches a
+// frame, the column prefixes 6 fewer).
+__device__ __forceinline__ void flag_publish(uint64_t* f, uint32_t epoch, uint32_t v) {
+    __hip_atomic_store(f, ((uint64_t)epoch << 32) | v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ uint32_t flag_wait(const uint64_t* f, uint32_t epoch) {
+    uint64_t x;
+    while (((x = __hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) >> 32) != epoch)
+        __builtin_amdgcn_s_sleep(1);
+    return (uint32_t)x;
+}
+// the block's count is published by its last thread; returns the sum of blocks [0, b)
+__device__ __forceinline__ int block_exclusive(uint64_t* flags, int b, uint32_t epoch, int total, int* s_base) {
+    if (threadIdx.x == SC_THREADS - 1) flag_publish(flags + b, epoch, (uint32_t)total);
+    int part = 0;
+    for (int i = threadIdx.x; i < b; i += SC_THREADS) part += (int)flag_wait(flags + i, epoch);
+    if (part) atomicAdd(s_base, part);
+    __syncthreads();
+    return *s_base;
 }
 
-// out_list[rank] = pixel of each outlier; dtmp = disp everywhere (the Jacobi output
-// starts as the input; the decision overwrites high-vote outliers).
-// Each block's first rank is the sum of the outlier counts of the blocks before it (read
-// and reduced here: a few hundred counts, no separate scan launch); the last block writes
-// the total.
-// rank[p] = the outliers before pixel p in raster order (rank[n] = all of them): the valid
-// pixels of a raster range [p0, p1] are then (p1 - p0 + 1) - (rank[p1 + 1] - rank[p0]).
-__global__ void k_oscan_scatter(const int32_t* __restrict__ disp, int n, int minD, const int32_t* __restrict__ bsum,
-                                int32_t* __restrict__ out_list, int32_t* __restrict__ dtmp,
-                                int32_t* __restrict__ counts, int32_t* __restrict__ rank, size_t ps) {
-    pair_shift(blockIdx.z, ps, disp, bsum, out_list, dtmp, counts, rank);
-    __shared__ int s_base;
-    if (threadIdx.x == 0) s_base = 0;
-    __syncthreads();
-    {
-        int part = 0;
-        for (int i = threadIdx.x; i < (int)blockIdx.x; i += SC_THREADS) part += bsum[2 * i];
-        if (part) atomicAdd(&s_base, part);
+// Valid-pixel counts of a voting pass's inner segments (valid: disp >= minD, the
+// reference's sample test :1122) as differences of prefix counts, exact integer arithmetic in
+// any order.  Rows (hf): the raster ranks.  Columns (!hf):
+//   P(y, x) = cpre[(y >> 5) W + x] + pre[y W + x], the valid pixels of column x at rows < y
+//   (y in [0, H]): pre holds the count inside 32-row chunks, cpre the counts of the chunks
+//   before.
+// vpre: rank[0 .. N], then pre[(H+1) W], then cpre[(H/32+2) W].
+constexpr int VP_CH = 32;
+size_t refine_vpre_ints(int H, int W) {
+    return (size_t)H * W + 1 + (size_t)(H + 1) * W + (size_t)(H / VP_CH + 2) * W;
+}
+__host__ __device__ inline size_t vpre_cols_off(int H, int W) { return (size_t)H * W + 1; }
+// 64-bit scan flags of a pair slot: the outlier ranking's blocks, the high-vote list's
+// blocks, then one per (32-row chunk, column)
+size_t refine_flag_words(int H, int W) {
+    return 2 * refine_scan_blocks(H * W) + (size_t)(H / VP_CH + 1) * W;
+}
+
+// One launch per voting pass before the counts, two roles by block index:
+//  * blocks [0, nb): the outliers' raster ranks.  out_list[rank] = pixel of each outlier;
+//    dtmp = disp everywhere (the Jacobi output starts as the input; the decision overwrites
+//    high-vote outliers); rank[p] = the outliers before pixel p in raster order (rank[n] =
+//    all of them): the valid pixels of a raster range [p0, p1] are then
+//    (p1 - p0 + 1) - (rank[p1 + 1] - rank[p0]).  The last block writes the totals.
+//  * blocks [nb, nb + ncx * nch) (vertical passes only): thread (chunk c, column x) counts
+//    the valid pixels of rows [32c, 32c + 32) into pre (local prefix), publishes the
+//    chunk's total and sums the chunks above it into cpre[c W + x].
+__global__ __launch_bounds__(SC_THREADS) void k_vote_prep(const int32_t* __restrict__ disp, int n, int nb,
+                                                          uint64_t* __restrict__ flags, int32_t* __restrict__ out_list,
+                                                          int32_t* __restrict__ dtmp, int32_t* __restrict__ counts,
+                                                          int32_t* __restrict__ rank, uint32_t epoch, DevParams Pk) {
+    const DevParams P = Pk;
+    pair_shift(blockIdx.z, P.pstride, disp, flags, out_list, dtmp, counts, rank);
+    const int minD = P.minD;
+    if ((int)blockIdx.x >= nb) {  // column prefixes
+        const int W = P.W, H = P.H;
+        const int ncx = (W + SC_THREADS - 1) / SC_THREADS;
+        const int j = (int)blockIdx.x - nb, c = j / ncx;
+        const int x = (j - c * ncx) * SC_THREADS + threadIdx.x;
+        if (x >= W) return;
+        int32_t* pre = rank + vpre_cols_off(H, W);
+        int32_t* cpre = pre + (size_t)(H + 1) * W;
+        uint64_t* cflag = flags + 2 * (size_t)nb;
+        const int y0 = c * VP_CH, y1 = min(H, y0 + VP_CH);
+        int run = 0;
+        int dv[VP_CH];
+#pragma unroll
+        for (int k = 0; k < VP_CH; ++k) dv[k] = y0 + k < y1 ? disp[(size_t)(y0 + k) * W + x] : -1;
+#pragma unroll
+        for (int k = 0; k < VP_CH; ++k) {
+            // rows y0 .. y1 - 1, and y = H in the chunk holding it (P's local part at y = H)
+            if (y0 + k < y1 || (y0 + k == H && H - y0 < VP_CH)) pre[(size_t)(y0 + k) * W + x] = run;
+            run += dv[k] >= minD ? 1 : 0;
+        }
+        flag_publish(cflag + (size_t)c * W + x, epoch, (uint32_t)run);
+        int above = 0;
+        for (int cc = 0; cc < c; ++cc) above += (int)flag_wait(cflag + (size_t)cc * W + x, epoch);
+        cpre[(size_t)c * W + x] = above;
+        return;
     }
     __shared__ int sa[SC_THREADS], sb[SC_THREADS];
+    __shared__ int s_base;
+    if (threadIdx.x == 0) s_base = 0;
     const int base = blockIdx.x * SC_BLOCK + threadIdx.x * SC_ITEMS;
     int dv[SC_ITEMS];
     load_items(disp, base, n, dv);
     int a = 0, b = 0;
 #pragma unroll
     for (int k = 0; k < SC_ITEMS; ++k) a += dv[k] < minD ? 1 : 0;
-    block_scan2(a, b, sa, sb);  // its barriers also publish s_base
-    const int first = s_base;
+    block_scan2(a, b, sa, sb);  // its barriers also publish s_base = 0
+    const int total = sa[SC_THREADS - 1];
+    const int first = block_exclusive(flags, blockIdx.x, epoch, total, &s_base);
     a += first;
-    if (threadIdx.x == SC_THREADS - 1 && blockIdx.x == gridDim.x - 1) {
-        counts[0] = first + sa[SC_THREADS - 1];
+    if (threadIdx.x == SC_THREADS - 1 && (int)blockIdx.x == nb - 1) {
+        counts[0] = first + total;
         counts[1] = 0;
         counts[2] = 0;  // the decision's long-carry list (k_vote_decide_wave)
-        rank[n] = first + sa[SC_THREADS - 1];
+        rank[n] = first + total;
     }
     {
         int rk = a;
@@ -193,63 +245,6 @@ __global__ void k_oscan_scatter(const int32_t* __restrict__ disp, int n, int min
 #pragma unroll
     for (int k = 0; k < SC_ITEMS; ++k)
         if (dv[k] < minD) out_list[a++] = base + k;
-}
-
-// Valid-pixel counts of a voting pass's inner segments (valid: disp >= minD, the
-// reference's sample test :1122) as differences of prefix counts, exact integer arithmetic in
-// any order.  Rows (hf): the raster ranks of k_oscan_scatter.  Columns (!hf):
-//   P(y, x) = cpre[(y >> 5) W + x] + pre[y W + x], the valid pixels of column x at rows < y
-//   (y in [0, H]): pre holds the count inside 32-row chunks, cpre the counts of the chunks
-//   before (two launches, W x H/32 threads).
-// vpre: rank[0 .. N], then pre[(H+1) W], then cpre[(H/32+2) W].
-constexpr int VP_CH = 32;
-size_t refine_vpre_ints(int H, int W) {
-    return (size_t)H * W + 1 + (size_t)(H + 1) * W + (size_t)(H / VP_CH + 2) * W;
-}
-__host__ __device__ inline size_t vpre_cols_off(int H, int W) { return (size_t)H * W + 1; }
-
-// columns, step 1: thread (chunk c, column x) counts inside rows [32c, 32c + 32); the chunk
-// holding row H also writes P's local part at y = H
-__global__ __launch_bounds__(256) void k_vprefix_cols(const int32_t* __restrict__ disp, int32_t* __restrict__ pre,
-                                                      DevParams Pk) {
-    const DevParams P = Pk;
-    pair_shift(blockIdx.z, P.pstride, disp, pre);
-    const int W = P.W, H = P.H;
-    pre += vpre_cols_off(H, W);
-    const int x = blockIdx.x * 256 + threadIdx.x, c = blockIdx.y;
-    if (x >= W) return;
-    int32_t* cpre = pre + (size_t)(H + 1) * W;
-    const int y0 = c * VP_CH, y1 = min(H, y0 + VP_CH);
-    int run = 0;
-    int dv[VP_CH];
-#pragma unroll
-    for (int k = 0; k < VP_CH; ++k) dv[k] = y0 + k < y1 ? disp[(size_t)(y0 + k) * W + x] : -1;
-#pragma unroll
-    for (int k = 0; k < VP_CH; ++k) {
-        if (y0 + k <= y1 && y0 + k <= H) {
-            if (y0 + k < H || (H - y0) < VP_CH) pre[(size_t)(y0 + k) * W + x] = run;
-        }
-        run += dv[k] >= P.minD ? 1 : 0;
-    }
-    cpre[(size_t)(c + 1) * W + x] = run;  // this chunk's total (scanned by step 2)
-}
-
-// columns, step 2: exclusive scan of the chunk totals per column (in place)
-__global__ __launch_bounds__(256) void k_vprefix_cols_scan(int32_t* __restrict__ pre, DevParams Pk) {
-    const DevParams P = Pk;
-    pair_shift(blockIdx.z, P.pstride, pre);
-    const int W = P.W, H = P.H;
-    pre += vpre_cols_off(H, W);
-    const int x = blockIdx.x * 256 + threadIdx.x;
-    if (x >= W) return;
-    int32_t* cpre = pre + (size_t)(H + 1) * W;
-    const int nc = H / VP_CH + 1;  // chunks holding rows 0 .. H
-    int run = 0;
-    for (int c = 0; c < nc; ++c) {
-        const int t = cpre[(size_t)(c + 1) * W + x];
-        cpre[(size_t)c * W + x] = run;
-        run += t;
-    }
 }
 
 // valid pixels of the inner segment at (yy0, xx0), offsets [-a2, b2] along the inner direction
@@ -343,55 +338,29 @@ __global__ __launch_bounds__(256) void k_vote_count_rank(const int32_t* __restri
 }
 
 // The high-vote outliers (vote > votingThresh, :1132) listed in rank order: hv_list[k] = the
-// rank of the k-th one, counts[1] = how many.  Two launches over the ranks, as the outlier
-// ranking (per-block counts in bsum[2 b + 1], then the scatter).
-__device__ __forceinline__ int hv_flags(const int32_t* __restrict__ cvote, int base, int nout, int thresh,
-                                        int (&f)[SC_ITEMS]) {
-    int c = 0;
-#pragma unroll
-    for (int k = 0; k < SC_ITEMS; ++k) {
-        f[k] = base + k < nout && cvote[base + k] > thresh ? 1 : 0;
-        c += f[k];
-    }
-    return c;
-}
-
-__global__ void k_hv_count(const int32_t* __restrict__ cvote, const int32_t* __restrict__ counts,
-                           int32_t* __restrict__ bsum, int thresh, size_t ps) {
-    pair_shift(blockIdx.z, ps, cvote, counts, bsum);
+// rank of the k-th one, counts[1] = how many.  One single-pass launch over the ranks, as the
+// outlier ranking (k_vote_prep): its own flags after the ranking's nb.
+__global__ __launch_bounds__(SC_THREADS) void k_hv_list(const int32_t* __restrict__ cvote, int32_t* __restrict__ counts,
+                                                        uint64_t* __restrict__ flags, int32_t* __restrict__ hv_list,
+                                                        int thresh, uint32_t epoch, size_t ps) {
+    pair_shift(blockIdx.z, ps, cvote, counts, flags, hv_list);
     __shared__ int sa[SC_THREADS], sb[SC_THREADS];
-    const int nout = counts[0];
-    const int base = blockIdx.x * SC_BLOCK + threadIdx.x * SC_ITEMS;
-    int f[SC_ITEMS];
-    int a = base < nout ? hv_flags(cvote, base, nout, thresh, f) : 0, b = 0;
-    block_scan2(a, b, sa, sb);
-    if (threadIdx.x == SC_THREADS - 1) bsum[2 * blockIdx.x + 1] = sa[SC_THREADS - 1];
-}
-
-__global__ void k_hv_scatter(const int32_t* __restrict__ cvote, int32_t* __restrict__ counts,
-                             const int32_t* __restrict__ bsum, int32_t* __restrict__ hv_list, int thresh, size_t ps) {
-    pair_shift(blockIdx.z, ps, cvote, counts, bsum, hv_list);
     __shared__ int s_base;
     if (threadIdx.x == 0) s_base = 0;
-    __syncthreads();
-    {
-        int part = 0;
-        for (int i = threadIdx.x; i < (int)blockIdx.x; i += SC_THREADS) part += bsum[2 * i + 1];
-        if (part) atomicAdd(&s_base, part);
-    }
-    __shared__ int sa[SC_THREADS], sb[SC_THREADS];
     const int nout = counts[0];
     const int base = blockIdx.x * SC_BLOCK + threadIdx.x * SC_ITEMS;
     int f[SC_ITEMS];
     int a = 0, b = 0;
-    if (base < nout) a = hv_flags(cvote, base, nout, thresh, f);
-    else {
 #pragma unroll
-        for (int k = 0; k < SC_ITEMS; ++k) f[k] = 0;
+    for (int k = 0; k < SC_ITEMS; ++k) {
+        f[k] = base + k < nout && cvote[base + k] > thresh ? 1 : 0;
+        a += f[k];
     }
-    block_scan2(a, b, sa, sb);  // its barriers also publish s_base
-    a += s_base;
-    if (threadIdx.x == SC_THREADS - 1 && blockIdx.x == gridDim.x - 1) counts[1] = s_base + sa[SC_THREADS - 1];
+    block_scan2(a, b, sa, sb);  // its barriers also publish s_base = 0
+    const int total = sa[SC_THREADS - 1];
+    const int first = block_exclusive(flags + gridDim.x, blockIdx.x, epoch, total, &s_base);
+    a += first;
+    if (threadIdx.x == SC_THREADS - 1 && blockIdx.x == gridDim.x - 1) counts[1] = first + total;
 #pragma unroll
     for (int k = 0; k < SC_ITEMS; ++k)
         if (f[k]) hv_list[a++] = base + k;
@@ -1071,28 +1040,22 @@ void launch_region_voting(RefineBufs& B, const uint32_t* arms0, int hf, const De
     const int n = P.H * P.W;
     const int nb = (int)refine_scan_blocks(n);
     const size_t ps = P.pstride;
-    hipLaunchKernelGGL(k_oscan_count, grid1d(nb, P), dim3(SC_THREADS), 0, st, B.dm, n, P.minD, B.bsum, ps);
-    trace_point("k_oscan_count", st);
-    hipLaunchKernelGGL(k_oscan_scatter, grid1d(nb, P), dim3(SC_THREADS), 0, st, B.dm, n, P.minD, B.bsum,
-                       B.out_list, B.dtmp, B.counts, B.vpre, ps);
-    trace_point("k_oscan_scatter", st);
-    if (!hf) {  // vertical inner segments: column prefix counts (rows use the raster ranks)
-        hipLaunchKernelGGL(k_vprefix_cols, dim3((P.W + 255) / 256, P.H / VP_CH + 1, P.npairs), dim3(256), 0, st,
-                           B.dm, B.vpre, P);
-        hipLaunchKernelGGL(k_vprefix_cols_scan, dim3((P.W + 255) / 256, 1, P.npairs), dim3(256), 0, st, B.vpre, P);
-        trace_point("k_vprefix_cols", st);
-    }
+    // one launch: the outlier ranking (nb blocks) and, for vertical inner segments, the column
+    // prefix counts (rows use the raster ranks)
+    const int ncol = hf ? 0 : ((P.W + SC_THREADS - 1) / SC_THREADS) * (P.H / VP_CH + 1);
+    const uint32_t ep = ++B.epoch;
+    hipLaunchKernelGGL(k_vote_prep, grid1d(nb + ncol, P), dim3(SC_THREADS), 0, st, B.dm, n, nb, B.flags, B.out_list,
+                       B.dtmp, B.counts, B.vpre, ep, P);
+    trace_point("k_vote_prep", st);
     // grid-stride over the ranked outliers (their count stays on the device)
     // latency-bound walks: single pairs take enough waves to keep every SIMD several deep
     const int vc_blocks = std::max(64, 4096 / std::max(1, P.npairs));
     hipLaunchKernelGGL(k_vote_count_rank, grid1d(vc_blocks, P), dim3(256), 0, st, B.dm, arms0, B.out_list,
                        B.counts, B.cvote, B.csamp, B.vpre, hf, P);
     trace_point("k_vote_count_rank", st);
-    hipLaunchKernelGGL(k_hv_count, grid1d(nb, P), dim3(SC_THREADS), 0, st, B.cvote, B.counts, B.bsum,
-                       P.voting_thresh, ps);
-    hipLaunchKernelGGL(k_hv_scatter, grid1d(nb, P), dim3(SC_THREADS), 0, st, B.cvote, B.counts, B.bsum, B.hv_list,
-                       P.voting_thresh, ps);
-    trace_point("k_hv_scatter", st);
+    hipLaunchKernelGGL(k_hv_list, grid1d(nb, P), dim3(SC_THREADS), 0, st, B.cvote, B.counts, B.flags, B.hv_list,
+                       P.voting_thresh, ep, ps);
+    trace_point("k_hv_list", st);
     // one wave per high-vote outlier, grid-stride; a histogram of L ints per wave
     const size_t lds = (size_t)VD_WAVES * P.L * sizeof(int);
     static_assert((size_t)VD_WAVES * 2048 * sizeof(int) <= 64 * 1024, "vote-decision LDS past the default limit");

@@ -67,7 +67,7 @@ struct RefineBufs {
     int32_t* out_list;// [H][W]
     int32_t* cvote;   // [H][W] vote count by outlier rank (out_pos order)
     uint16_t* csamp;  // [H][W][20] low-vote samples by outlier rank
-    int32_t* bsum;    // scan block sums [2 * nblocks]
+    uint64_t* flags;  // single-pass scan flags (epoch << 32 | count), refine_flag_words
     int32_t* hv_list; // [H][W] ranks of the high-vote outliers of a voting pass, in rank order
     int32_t* long_list; // [H][W] indices into hv_list of the ranks with long carries
     int32_t* counts;  // [4]
@@ -84,10 +84,13 @@ struct RefineBufs {
     uint8_t* edges;   // [H][W]
     float* subpix;    // [H][W]
     int32_t* vpre;    // valid-pixel prefix counts of a voting pass (refine_vpre_ints)
+    uint32_t epoch = 0;  // voting launches so far on this workspace (tags the scan flags)
 };
 // ints of RefineBufs.vpre: raster ranks (H W + 1), column prefixes ((H+1) W + chunk prefixes)
 size_t refine_vpre_ints(int H, int W);
 size_t refine_scan_blocks(int n);
+// 64-bit words of RefineBufs.flags
+size_t refine_flag_words(int H, int W);
 void launch_outlier(RefineBufs& B, const DevParams& P, hipStream_t st);
 void launch_region_voting(RefineBufs& B, const uint32_t* arms0, int horizontal_first,
                           const DevParams& P, hipStream_t st);
