@@ -396,9 +396,9 @@ __global__ __launch_bounds__(AX_THREADS) void k_agg_split(AggStream S, DevParams
     const __amdgpu_buffer_rsrc_t rs_vol = make_rsrc(volq);
     auto store = [&](uint32_t lo, uint32_t hi, const f32x4& acc) {
         if (!vl) return;
-        if (BIG) {
+        if (BIG) {  // plain stores (configs C / E: non-temporal ones measured 2 % slower on C, round 6)
             const size_t o = ((size_t)hi << 32 | lo) >> 2;
-            st_stream(volq + o + 4 * lane, acc);
+            *reinterpret_cast<f32x4*>(volq + o + 4 * lane) = acc;
         } else {
             __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, acc), rs_vol, lane16, lo, 2);
         }

@@ -90,7 +90,9 @@ __global__ void k_gauss_median(const uint32_t* __restrict__ src, uint32_t* __res
 // ---------------------------------------------------------------------------
 // census descriptors: desc[v][y][x][16]
 //   RGB: words 0..5 = gt planes (ch0 lo,hi, ch1 lo,hi, ch2 lo,hi), 6..11 = lt planes
-//   HSI: words 0..1 = hue "positive" plane, 2..5 = sat/int gt, 6..9 = sat/int lt
+//   HSI: words 0..1 = hue "positive" plane, 2..5 = sat/int gt, 6..9 = sat/int lt,
+//        10 = the hue byte alone, 11 = the sat / int bytes alone (the AD term's two sums
+//        without per-cell masks in the walk)
 //   word 12 = the pixel's packed colour (AD term, mask tests), words 13..15 = 0.
 // One 64-B record per pixel, so the cost walk fetches a whole record with one scalar
 // load.  Border pixels (window leaving the image) never reach the cost (:562-566):
@@ -156,6 +158,10 @@ __global__ __launch_bounds__(CD_TX) void k_census_desc(const uint32_t* __restric
         }
     }
     u32x4* o = reinterpret_cast<u32x4*>(desc + (((size_t)v * H + y) * W + x) * 16);
+    if (HSI) {
+        w[10] = c & 0xffu;
+        w[11] = c & 0xffff00u;
+    }
     o[0] = u32x4{w[0], w[1], w[2], w[3]};
     o[1] = u32x4{w[4], w[5], w[6], w[7]};
     o[2] = u32x4{w[8], w[9], w[10], w[11]};
@@ -211,9 +217,11 @@ __device__ __forceinline__ uint32_t bcnt_acc(uint32_t x, uint32_t acc) {
 // requires, doubled: the table holds k / 2): 2 * circular hue distance + 5 * (|dS| + |dI|),
 // the factor 5 as a 24-bit multiply (the compiler otherwise picks the quarter-rate
 // v_mul_lo_u32)
-__device__ __forceinline__ int hsi_ad(uint32_t fc, uint32_t vc) {
-    const uint32_t hd = __builtin_amdgcn_sad_u8(fc & 0xffu, vc & 0xffu, 0u);
-    const uint32_t si = __builtin_amdgcn_sad_u8(fc & 0xffff00u, vc & 0xffff00u, 0u);
+// The records carry the hue byte and the sat / int bytes as separate words (10, 11), so
+// neither sum needs a mask.
+__device__ __forceinline__ int hsi_ad(uint32_t fh, uint32_t fsi, uint32_t vh, uint32_t vsi) {
+    const uint32_t hd = __builtin_amdgcn_sad_u8(fh, vh, 0u);
+    const uint32_t si = __builtin_amdgcn_sad_u8(fsi, vsi, 0u);
     return (int)(2u * min(hd, 255u - hd) + __umul24(si, 5u));
 }
 
@@ -265,7 +273,9 @@ __global__ __launch_bounds__(CW_THREADS) __attribute__((amdgpu_waves_per_eu(E ==
     const int vtop = E * 64 - 1;  // view 1 feeds its shift register at the top label
     const int hw = P.censusW >> 1, hh = P.censusH >> 1;
     const bool rowOut = y - hh < 0 || y + hh >= H;
-    constexpr int NW = HSI ? 11 : 13;  // shifted words: descriptor planes + colour
+    // shifted words: RGB the 12 descriptor planes + the colour (word 12); HSI the 10 planes +
+    // the hue and sat / int words (10, 11).  Either way word w of a record.
+    constexpr int NW = HSI ? 12 : 13;
     constexpr int CWORD = 12;          // colour word of a record
     const uint32_t vmask_hi = (P.censusW * P.censusH - 1) >= 64
                                   ? 0xffffffffu
@@ -322,14 +332,14 @@ __global__ __launch_bounds__(CW_THREADS) __attribute__((amdgpu_waves_per_eu(E ==
         const u32x4 a = r[0], b = r[1], c = r[2], d = r[3];
         const uint32_t rec[13] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w, c.x, c.y, c.z, c.w, d.x};
 #pragma unroll
-        for (int w = 0; w < NW; ++w) V[w][e] = rec[w < NW - 1 ? w : CWORD];
+        for (int w = 0; w < NW; ++w) V[w][e] = rec[w];
     }
 
     // record -> NW shifted words (descriptor planes, then the colour)
     auto pick = [&](const u32x4& a, const u32x4& b, const u32x4& c, const u32x4& d, uint32_t (&o)[NW]) {
         const uint32_t rec[13] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w, c.x, c.y, c.z, c.w, d.x};
 #pragma unroll
-        for (int w = 0; w < NW; ++w) o[w] = rec[w < NW - 1 ? w : CWORD];
+        for (int w = 0; w < NW; ++w) o[w] = rec[w];
     };
     auto load_staged = [&](const u32x4* st, int t, uint32_t (&o)[NW]) {
         const int i = t * 4;
@@ -373,12 +383,11 @@ __global__ __launch_bounds__(CW_THREADS) __attribute__((amdgpu_waves_per_eu(E ==
 #pragma unroll
                         for (int w = 2; w < 6; ++w) cen = bcnt_acc((Fr[w] & Vr[4 + w]) | (Fr[4 + w] & Vr[w]), cen);
                     }
-                    const uint32_t vc = Vr[NW - 1], fc = Fr[NW - 1];
                     int ai;
                     if (!HSI) {
-                        ai = (int)__builtin_amdgcn_sad_u8(fc, vc, 0u);
+                        ai = (int)__builtin_amdgcn_sad_u8(Fr[NW - 1], Vr[NW - 1], 0u);
                     } else {
-                        ai = hsi_ad(fc, vc);
+                        ai = hsi_ad(Fr[10], Fr[11], Vr[10], Vr[11]);
                     }
                     const float c = sA[ai] - sB[cen];
                     c4[t] = (fixed_ok && k >= klo && k <= khi) ? c : 2.f;
@@ -451,12 +460,16 @@ __global__ __launch_bounds__(CW_THREADS) __attribute__((amdgpu_waves_per_eu(E ==
 #pragma unroll
         for (int e = 0; e < E; ++e) {
             const int s = UP ? (e - R + E) % E : (e + R) % E;
-            const uint32_t vc = V[NW - 1][s], fc = F[NW - 1];
             int ai;
+            uint32_t fc, vc;  // the packed colours (mask tests)
             if (!HSI) {
+                fc = F[NW - 1];
+                vc = V[NW - 1][s];
                 ai = (int)__builtin_amdgcn_sad_u8(fc, vc, 0u);
             } else {
-                ai = hsi_ad(fc, vc);
+                fc = F[10] | F[11];
+                vc = V[10][s] | V[11][s];
+                ai = hsi_ad(F[10], F[11], V[10][s], V[11][s]);
             }
             // mask mode: black centre on either side -> census = +inf (:459-460)
             if (MASK && (fc == 0 || vc == 0)) cen[e] = 187;
