@@ -337,10 +337,6 @@ void layout_slot(Workspace* w, SlotLayout& S, int H, int W, int L, int model) {
     S.take(B.gray, N);
     S.take(B.gray_eq, N);
     S.take(B.hist, (256 + 64) * 4);
-    S.take(B.blurred, N);
-    S.take(B.dx, N * 2);
-    S.take(B.dy, N * 2);
-    S.take(B.mag, N * 4);
     S.take(B.map, N);
     S.take(B.label, N * 4);
     S.take(B.strong, N);
@@ -700,11 +696,10 @@ int run_pipeline(tsm_adc* h, Workspace* w, int K, const PairIn& in, size_t step,
     launch_interpolation(w->rb, w->img, P, st);
     if (dump && dump->interp && (rc = d2h(dump->interp, w->rb.dm, N * 4)) != TSM_OK) return rc;
     launch_discontinuity(w->rb, w->vol, P, st);
+    launch_refine_tail(w->rb, w->vol, w->img_orig, outs, out_step, (h->roi || h->mask) ? 1 : 0, h->offset, P, st);
     if (dump && dump->gray && (rc = d2h(dump->gray, w->rb.gray_eq, N)) != TSM_OK) return rc;
     if (dump && dump->edges && (rc = d2h(dump->edges, w->rb.edges, N)) != TSM_OK) return rc;
     if (dump && dump->adjusted && (rc = d2h(dump->adjusted, w->rb.dm, N * 4)) != TSM_OK) return rc;
-    launch_subpixel_median(w->rb, w->vol, w->img_orig, outs, out_step, (h->roi || h->mask) ? 1 : 0,
-                           h->offset, P, st);
     if (dump && dump->subpix && (rc = d2h(dump->subpix, w->rb.subpix, N * 4)) != TSM_OK) return rc;
     mark_stage();
     HIP_OK(hipGetLastError());

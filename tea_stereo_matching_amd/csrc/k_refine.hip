@@ -23,14 +23,8 @@
 namespace tsm {
 
 constexpr int kMaxSamples = 20; // = votingThresh: a low-vote outlier holds <= 20 samples
-
-// zero-fill on the stream by a kernel (keeps every producer/consumer inside the
-// kernel-ordering domain; no DMA-engine writes between kernels)
-__global__ void k_zero_u32(uint32_t* __restrict__ p, int n, size_t ps) {
-    pair_shift(blockIdx.z, ps, p);
-    const int i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i < n) p[i] = 0u;
-}
+// RefineBufs.hist: the discontinuity stage's 256-bin histogram (+ 64 spare ints)
+constexpr int kHistInts = 256 + 64;
 
 // ---------------------------------------------------------------------------
 // outlier elimination (LR check)
@@ -40,9 +34,12 @@ __global__ void k_zero_u32(uint32_t* __restrict__ p, int n, size_t ps) {
 // dR(x - k) == k?) asks whether any right-view pixel c maps onto x (c + dR(c) == x), so
 // each row scatters that map into an LDS bitmap once and every pixel tests one byte.
 __global__ __launch_bounds__(256) void k_outlier_row(const int32_t* __restrict__ dl, const int32_t* __restrict__ dr,
-                                                     int32_t* __restrict__ out, DevParams Pk) {
+                                                     int32_t* __restrict__ out, int32_t* __restrict__ hist, DevParams Pk) {
     const DevParams P = Pk;
-    pair_shift(blockIdx.z, P.pstride, dl, dr, out);
+    pair_shift(blockIdx.z, P.pstride, dl, dr, out, hist);
+    // the discontinuity stage's histogram, LUT and arrival counter start at zero
+    if (blockIdx.x == 0)
+        for (int k = threadIdx.x; k < kHistInts; k += blockDim.x) hist[k] = 0;
     extern __shared__ uint8_t hit[];
     const int y = blockIdx.x;
     const int W = P.W;
@@ -637,52 +634,49 @@ __global__ __launch_bounds__(256) void k_interp_rays(const int32_t* __restrict__
 }
 
 // ---------------------------------------------------------------------------
-// discontinuity adjustment: gray -> equalizeHist -> blur -> Canny -> adjust
+// discontinuity adjustment: gray -> equalizeHist -> blur -> Canny -> adjust, then subpixel +
+// median.  Round 6: 14 launches -> 6 (the hist zeroing rides on k_outlier_row, the LUT is
+// built by each block of the Canny launch, equalisation + blur + Sobel + NMS share one tiled launch, and the edge
+// test, the adjustment, the subpixel step and the median another): every stage keeps its
+// own arithmetic, so the outputs are the same bytes.
 // ---------------------------------------------------------------------------
-__global__ void k_gray_hist(const int32_t* __restrict__ disp, uint8_t* __restrict__ gray,
-                            int32_t* __restrict__ hist, int n, size_t ps) {
+// gray = (uchar)max(d, 0) (:1249, wraps > 255) and its histogram (the LUT is built by every
+// block of k_canny_front from it: a last-block LUT here needed a device-scope fence in every
+// block, which wrote the gray bytes back out of L2 -- 67 against 15 us, round 6)
+__global__ __launch_bounds__(256) void k_gray_hist(const int32_t* __restrict__ disp, uint8_t* __restrict__ gray,
+                                                   int32_t* __restrict__ hist, int n, size_t ps) {
     pair_shift(blockIdx.z, ps, disp, gray, hist);
     __shared__ int h[256];
-    h[threadIdx.x] = 0;
+    const int k = threadIdx.x;
+    h[k] = 0;
     __syncthreads();
-    for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
+    for (int i = blockIdx.x * blockDim.x + k; i < n; i += gridDim.x * blockDim.x) {
         const int d = disp[i];
-        const uint8_t g = d < 0 ? 0 : (uint8_t)d; // (uchar) wraps > 255 (:1249)
+        const uint8_t g = d < 0 ? 0 : (uint8_t)d;  // (uchar) wraps > 255 (:1249)
         gray[i] = g;
         atomicAdd(&h[g], 1);
     }
     __syncthreads();
-    if (h[threadIdx.x]) atomicAdd(&hist[threadIdx.x], h[threadIdx.x]);
+    if (h[k]) atomicAdd(&hist[k], h[k]);
 }
 
-__device__ __forceinline__ int reflect101(int i, int n) {
-    if (n == 1) return 0;
-    if (i < 0) i = -i;
-    if (i >= n) i = 2 * n - 2 - i;
-    return i;
-}
-
-// equalizeHist LUT (imgproc histogram.cpp): lut[i] = saturate_cast<uchar>(sum * scale),
-// scale = 255.f / (total - hist[first nonzero]).  One 256-thread block: the running sums
-// are integers (an LDS prefix scan is exact), each entry then one multiply and rint.
-__global__ __launch_bounds__(256) void k_eq_lut(const int32_t* __restrict__ hist, uint8_t* __restrict__ lut_out,
-                                                int total, size_t ps) {
-    pair_shift(blockIdx.z, ps, hist, lut_out);
-    __shared__ int pre[256];
-    __shared__ int first;
+// equalizeHist LUT (imgproc histogram.cpp) entry k of a 256-thread block: lut[i] =
+// saturate_cast<uchar>(sum * scale), scale = 255.f / (total - hist[first nonzero]), from an
+// exact integer prefix scan in LDS
+__device__ __forceinline__ uint8_t eq_lut_entry(const int32_t* __restrict__ hist, int total, int* pre, int* first) {
     const int k = threadIdx.x;
     const int hk = hist[k];
     pre[k] = hk;
-    if (k == 0) first = 256;
+    if (k == 0) *first = 256;
     __syncthreads();
-    if (hk != 0) atomicMin(&first, k);
+    if (hk != 0) atomicMin(first, k);
     for (int off = 1; off < 256; off <<= 1) {  // inclusive prefix sums
         const int add = k >= off ? pre[k - off] : 0;
         __syncthreads();
         pre[k] += add;
         __syncthreads();
     }
-    const int i = first;
+    const int i = *first;
     uint8_t out = 0;
     if (i < 256) {
         const int hi = pre[i] - (i > 0 ? pre[i - 1] : 0);
@@ -695,72 +689,96 @@ __global__ __launch_bounds__(256) void k_eq_lut(const int32_t* __restrict__ hist
             out = (uint8_t)(v < 0 ? 0 : (v > 255 ? 255 : v));
         }
     }
-    lut_out[k] = out;
+    return out;
 }
 
-// blur 3x3 BORDER_REFLECT_101 of the equalised map with the ColumnSum<ushort,uchar>
-// fixed-point divide ((s+4)*932068)>>23 == round(s/9).
-__global__ void k_eq_blur(const uint8_t* __restrict__ gray, const uint8_t* __restrict__ lut_g,
-                          uint8_t* __restrict__ eq_out, uint8_t* __restrict__ blurred, int H, int W, size_t ps) {
-    pair_shift(blockIdx.z, ps, gray, lut_g, eq_out, blurred);
+__device__ __forceinline__ int reflect101(int i, int n) {
+    if (n == 1) return 0;
+    if (i < 0) i = -i;
+    if (i >= n) i = 2 * n - 2 - i;
+    return i;
+}
+
+// Canny front end on a TX x TY tile: the equalisation LUT (each block builds it from the
+// histogram) -> the equalised map -> blur 3x3 BORDER_REFLECT_101
+// with the ColumnSum<ushort,uchar> fixed-point divide ((s+4)*932068)>>23 == round(s/9) -> Sobel
+// 3x3 (BORDER_REPLICATE), L1 magnitude -> non-maximum suppression (canny.cpp TG22 fixed point,
+// zero magnitude outside the image).  Each stage runs on the tile plus the halo the next
+// needs (3, 2, 1 pixels), in LDS.  map: 1 = not an edge, 0 = weak candidate, 2 = strong
+// (m > high).  Also writes the equalised map (debug dumps) and zeroes the hysteresis's
+// strong-root bytes.
+constexpr int CF_TX = 32, CF_TY = 8;
+__global__ __launch_bounds__(256) void k_canny_front(const uint8_t* __restrict__ gray, const int32_t* __restrict__ hist,
+                                                     uint8_t* __restrict__ eq_out, uint8_t* __restrict__ map,
+                                                     uint8_t* __restrict__ strong, int H, int W, int low, int high,
+                                                     size_t ps) {
+    pair_shift(blockIdx.z, ps, gray, hist, eq_out, map, strong);
+    constexpr int EW = CF_TX + 6, EH = CF_TY + 6;  // equalised: halo 3
+    constexpr int BW = CF_TX + 4, BH = CF_TY + 4;  // blurred: halo 2
+    constexpr int SW = CF_TX + 2, SH = CF_TY + 2;  // Sobel: halo 1
     __shared__ uint8_t lut[256];
-    lut[threadIdx.x] = lut_g[threadIdx.x];
+    __shared__ int pre[256];
+    __shared__ int first;
+    __shared__ uint8_t se[EH][EW];
+    __shared__ uint8_t sbl[BH][BW];
+    __shared__ int smag[SH][SW];
+    __shared__ int16_t sdx[SH][SW], sdy[SH][SW];
+    const int x0 = blockIdx.x * CF_TX, y0 = blockIdx.y * CF_TY;
+    const int t = threadIdx.x;
+    lut[t] = eq_lut_entry(hist, H * W, pre, &first);
     __syncthreads();
-    const int x = blockIdx.x * blockDim.x + threadIdx.x;
-    const int y = blockIdx.y;
-    if (x >= W) return;
-    int s = 0;
-    for (int dy = -1; dy <= 1; ++dy) {
-        const int yy = reflect101(y + dy, H);
-        for (int dx = -1; dx <= 1; ++dx) s += lut[gray[(size_t)yy * W + reflect101(x + dx, W)]];
+    // region coordinates: e(r, c) is image (y0 - 3 + r, x0 - 3 + c); only in-image cells are
+    // ever read (reflect101 / clamps land inside the image, and inside these regions)
+    for (int k = t; k < EH * EW; k += 256) {
+        const int r = k / EW, c = k - r * EW;
+        const int yy = y0 - 3 + r, xx = x0 - 3 + c;
+        se[r][c] = (yy >= 0 && yy < H && xx >= 0 && xx < W) ? lut[gray[(size_t)yy * W + xx]] : 0;
     }
-    blurred[(size_t)y * W + x] = (uint8_t)(((s + 4) * 932068) >> 23);
-    if (eq_out) eq_out[(size_t)y * W + x] = lut[gray[(size_t)y * W + x]];
-}
-
-// Sobel 3x3 (BORDER_REPLICATE) -> dx, dy (CV_16S), L1 magnitude.
-__global__ void k_sobel(const uint8_t* __restrict__ src, int16_t* __restrict__ dx,
-                        int16_t* __restrict__ dy, int32_t* __restrict__ mag, int H, int W, size_t ps) {
-    pair_shift(blockIdx.z, ps, src, dx, dy, mag);
-    const int x = blockIdx.x * blockDim.x + threadIdx.x;
-    const int y = blockIdx.y;
-    if (x >= W) return;
-    auto S = [&](int yy, int xx) -> int {
-        yy = yy < 0 ? 0 : (yy >= H ? H - 1 : yy);
-        xx = xx < 0 ? 0 : (xx >= W ? W - 1 : xx);
-        return src[(size_t)yy * W + xx];
-    };
-    const int gx = (S(y - 1, x + 1) + 2 * S(y, x + 1) + S(y + 1, x + 1)) -
-                   (S(y - 1, x - 1) + 2 * S(y, x - 1) + S(y + 1, x - 1));
-    const int gy = (S(y + 1, x - 1) + 2 * S(y + 1, x) + S(y + 1, x + 1)) -
-                   (S(y - 1, x - 1) + 2 * S(y - 1, x) + S(y - 1, x + 1));
-    const size_t i = (size_t)y * W + x;
-    dx[i] = (int16_t)gx;
-    dy[i] = (int16_t)gy;
-    mag[i] = abs(gx) + abs(gy);
-}
-
-// Non-maximum suppression (canny.cpp TG22 fixed point, zero magnitude outside the image).
-// map: 1 = not an edge, 0 = weak candidate, 2 = strong (m > high).
-__global__ void k_nms(const int16_t* __restrict__ dx, const int16_t* __restrict__ dy,
-                      const int32_t* __restrict__ mag, uint8_t* __restrict__ map, int H, int W,
-                      int low, int high, size_t ps) {
-    pair_shift(blockIdx.z, ps, dx, dy, mag, map);
-    const int x = blockIdx.x * blockDim.x + threadIdx.x;
-    const int y = blockIdx.y;
-    if (x >= W) return;
+    __syncthreads();
+    for (int k = t; k < BH * BW; k += 256) {
+        const int r = k / BW, c = k - r * BW;
+        const int y = y0 - 2 + r, x = x0 - 2 + c;
+        if (y < 0 || y >= H || x < 0 || x >= W) continue;
+        int s = 0;
+        for (int dy = -1; dy <= 1; ++dy) {
+            const int yy = reflect101(y + dy, H) - (y0 - 3);
+            for (int dx = -1; dx <= 1; ++dx) s += se[yy][reflect101(x + dx, W) - (x0 - 3)];
+        }
+        sbl[r][c] = (uint8_t)(((s + 4) * 932068) >> 23);
+    }
+    __syncthreads();
+    for (int k = t; k < SH * SW; k += 256) {
+        const int r = k / SW, c = k - r * SW;
+        const int y = y0 - 1 + r, x = x0 - 1 + c;
+        if (y < 0 || y >= H || x < 0 || x >= W) continue;
+        auto S = [&](int yy, int xx) -> int {
+            yy = yy < 0 ? 0 : (yy >= H ? H - 1 : yy);
+            xx = xx < 0 ? 0 : (xx >= W ? W - 1 : xx);
+            return sbl[yy - (y0 - 2)][xx - (x0 - 2)];
+        };
+        const int gx = (S(y - 1, x + 1) + 2 * S(y, x + 1) + S(y + 1, x + 1)) -
+                       (S(y - 1, x - 1) + 2 * S(y, x - 1) + S(y + 1, x - 1));
+        const int gy = (S(y + 1, x - 1) + 2 * S(y + 1, x) + S(y + 1, x + 1)) -
+                       (S(y - 1, x - 1) + 2 * S(y - 1, x) + S(y - 1, x + 1));
+        sdx[r][c] = (int16_t)gx;
+        sdy[r][c] = (int16_t)gy;
+        smag[r][c] = abs(gx) + abs(gy);
+    }
+    __syncthreads();
+    const int x = x0 + (t % CF_TX), y = y0 + t / CF_TX;
+    if (x >= W || y >= H) return;
     auto M = [&](int yy, int xx) -> int {
         if (yy < 0 || yy >= H || xx < 0 || xx >= W) return 0;
-        return mag[(size_t)yy * W + xx];
+        return smag[yy - (y0 - 1)][xx - (x0 - 1)];
     };
-    const size_t i = (size_t)y * W + x;
-    const int m = mag[i];
+    const int r = y - (y0 - 1), c = x - (x0 - 1);
+    const int m = smag[r][c];
     bool keep = false;
     if (m > low) {
-        const int xs = dx[i], ys = dy[i];
+        const int xs = sdx[r][c], ys = sdy[r][c];
         const int ax = abs(xs);
         const int ay = abs(ys) << 15;
-        const int tg22x = ax * 13573; // (int)(0.4142135623730950488 * (1 << 15) + 0.5)
+        const int tg22x = ax * 13573;  // (int)(0.4142135623730950488 * (1 << 15) + 0.5)
         if (ay < tg22x) {
             keep = m > M(y, x - 1) && m >= M(y, x + 1);
         } else {
@@ -773,7 +791,10 @@ __global__ void k_nms(const int16_t* __restrict__ dx, const int16_t* __restrict_
             }
         }
     }
+    const size_t i = (size_t)y * W + x;
     map[i] = !keep ? 1 : (m > high ? 2 : 0);
+    eq_out[i] = se[y - (y0 - 3)][x - (x0 - 3)];
+    strong[i] = 0;
 }
 
 // Hysteresis = 8-connected components of {map != 1} containing a strong pixel.
@@ -887,28 +908,15 @@ __global__ void k_uf_flatten_mark(const uint8_t* __restrict__ map, int32_t* __re
     if (map[i] == 2) strong[r] = 1;
 }
 
-__global__ void k_uf_final(const uint8_t* __restrict__ map, const int32_t* __restrict__ label,
-                           const uint8_t* __restrict__ strong, uint8_t* __restrict__ edges, int n, size_t ps) {
-    pair_shift(blockIdx.z, ps, map, label, strong, edges);
-    const int i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= n) return;
-    edges[i] = (map[i] != 1 && strong[label[i]]) ? 255 : 0;
-}
-
-// discontinuityAdjustment body (:1266-1339); reads the pre-adjust map, writes dtmp.
-__global__ void k_adjust(const int32_t* __restrict__ disp, int32_t* __restrict__ out,
-                         const uint8_t* __restrict__ edges, const float* __restrict__ vol0,
-                         DevParams Pk) {
-    const DevParams P = Pk;  // kernel args -> registers once (no per-use kernarg reloads)
-    pair_shift(blockIdx.z, P.pstride, disp, out, edges, vol0);
-    const int x = blockIdx.x * blockDim.x + threadIdx.x;
-    const int y = blockIdx.y;
+// discontinuityAdjustment body (:1266-1339) for pixel (x, y) of the pre-adjust map; E(yy, xx):
+// the Canny edge test of a neighbour
+template <class EF>
+__device__ __forceinline__ int adjust_px(const int32_t* __restrict__ disp, const float* __restrict__ vol0, int x, int y,
+                                         const DevParams& P, EF E) {
     const int H = P.H, W = P.W, minD = P.minD, Lp = P.Lp;
-    if (x >= W) return;
     const size_t i = (size_t)y * W + x;
     int res = disp[i];
-    if (y >= 1 && y < H - 1 && x >= 1 && x < W - 1 && edges[i]) {
-        auto E = [&](int yy, int xx) -> bool { return edges[(size_t)yy * W + xx] != 0; };
+    if (y >= 1 && y < H - 1 && x >= 1 && x < W - 1 && E(y, x)) {
         int direction = -1;
         if (E(y - 1, x - 1) && E(y + 1, x + 1)) direction = 0;
         else if (E(y - 1, x + 1) && E(y + 1, x - 1)) direction = 4;
@@ -938,28 +946,20 @@ __global__ void k_adjust(const int32_t* __restrict__ disp, int32_t* __restrict__
             res = dsel;
         }
     }
-    out[i] = res;
+    return res;
 }
 
-// subpixelEnhancement (:1344-1370)
-__global__ void k_subpix(const int32_t* __restrict__ disp, const float* __restrict__ vol0,
-                         float* __restrict__ sub, DevParams Pk) {
-    const DevParams P = Pk;  // kernel args -> registers once (no per-use kernarg reloads)
-    pair_shift(blockIdx.z, P.pstride, disp, vol0, sub);
-    const int x = blockIdx.x * blockDim.x + threadIdx.x;
-    const int y = blockIdx.y;
-    const int W = P.W, minD = P.minD, Lp = P.Lp;
-    if (x >= W) return;
-    const size_t i = (size_t)y * W + x;
-    const int d = disp[i];
+// subpixelEnhancement (:1344-1374) of pixel i at disparity d
+__device__ __forceinline__ float subpix_px(const float* __restrict__ vol0, size_t i, int d, const DevParams& P) {
     float inter = (float)d;
     if (d > P.minD && d < P.maxD) {
-        const float* c = vol0 + i * Lp;
+        const float* c = vol0 + i * P.Lp;
+        const int minD = P.minD;
         const float c0 = c[d - minD], cp = c[d + 1 - minD], cm = c[d - 1 - minD];
         const float diff = (cp - cm) / (2 * (cp + cm - 2 * c0));
         if (diff > -1 && diff < 1) inter -= diff;
     }
-    sub[i] = inter;
+    return inter;
 }
 
 __device__ __forceinline__ void sort2(float& a, float& b) {
@@ -968,20 +968,62 @@ __device__ __forceinline__ void sort2(float& a, float& b) {
     b = hi;
 }
 
-// medianBlur 3x3 CV_32F (BORDER_REPLICATE) + ROI/mask post-processing (:388-403) + store.
-__global__ void k_median_out(const float* __restrict__ sub, PairOut outs,
-                             size_t out_step, const uint32_t* __restrict__ orig_left,
-                             int roi_or_mask, int offset, int H, int W, size_t ps) {
+// The refinement's last steps on a TX x TY tile: the edge map (hysteresis: a non-suppressed
+// pixel whose component holds a strong one) on the tile + 2, the discontinuity adjustment and
+// the subpixel step on the tile + 1, then medianBlur 3x3 CV_32F (BORDER_REPLICATE) + the ROI /
+// mask post-processing (:388-403) and the store.  Also writes the edge map, the adjusted map
+// (dtmp) and the subpixel map (debug dumps).
+constexpr int RT_TX = 32, RT_TY = 8;
+__global__ __launch_bounds__(256) void k_refine_tail(const uint8_t* __restrict__ map, const int32_t* __restrict__ label,
+                                                     const uint8_t* __restrict__ strong, uint8_t* __restrict__ edges,
+                                                     const int32_t* __restrict__ disp, int32_t* __restrict__ adj,
+                                                     const float* __restrict__ vol0, float* __restrict__ sub,
+                                                     PairOut outs, size_t out_step, const uint32_t* __restrict__ orig_left,
+                                                     int roi_or_mask, int offset, DevParams Pk) {
+    const DevParams P = Pk;
     float* out = outs.out[blockIdx.z];
-    pair_shift(blockIdx.z, ps, sub, orig_left);
-    const int x = blockIdx.x * blockDim.x + threadIdx.x;
-    const int y = blockIdx.y;
-    if (x >= W) return;
+    pair_shift(blockIdx.z, P.pstride, map, label, strong, edges, disp, adj, vol0, sub, orig_left);
+    constexpr int EW = RT_TX + 4, EH = RT_TY + 4;  // edges: halo 2
+    constexpr int AW = RT_TX + 2, AH = RT_TY + 2;  // adjusted + subpixel: halo 1
+    __shared__ uint8_t se[EH][EW];
+    __shared__ float ss[AH][AW];
+    const int H = P.H, W = P.W;
+    const int x0 = blockIdx.x * RT_TX, y0 = blockIdx.y * RT_TY;
+    const int t = threadIdx.x;
+    for (int k = t; k < EH * EW; k += 256) {
+        const int r = k / EW, c = k - r * EW;
+        const int yy = y0 - 2 + r, xx = x0 - 2 + c;
+        uint8_t e = 0;
+        if (yy >= 0 && yy < H && xx >= 0 && xx < W) {
+            const size_t i = (size_t)yy * W + xx;
+            e = (map[i] != 1 && strong[label[i]]) ? 255 : 0;
+        }
+        se[r][c] = e;
+    }
+    __syncthreads();
+    auto E = [&](int yy, int xx) -> bool { return se[yy - (y0 - 2)][xx - (x0 - 2)] != 0; };
+    for (int k = t; k < AH * AW; k += 256) {
+        const int r = k / AW, c = k - r * AW;
+        const int y = y0 - 1 + r, x = x0 - 1 + c;
+        if (y < 0 || y >= H || x < 0 || x >= W) continue;
+        const int a = adjust_px(disp, vol0, x, y, P, E);
+        const size_t i = (size_t)y * W + x;
+        const float s = subpix_px(vol0, i, a, P);
+        ss[r][c] = s;
+        if (r >= 1 && r <= RT_TY && c >= 1 && c <= RT_TX) {  // the tile's own pixels
+            adj[i] = a;
+            sub[i] = s;
+            edges[i] = se[r + 1][c + 1];
+        }
+    }
+    __syncthreads();
+    const int x = x0 + (t % RT_TX), y = y0 + t / RT_TX;
+    if (x >= W || y >= H) return;
     float v[9];
     int k = 0;
     for (int dy = -1; dy <= 1; ++dy) {
-        const int yy = min(max(y + dy, 0), H - 1);
-        for (int dx = -1; dx <= 1; ++dx) v[k++] = sub[(size_t)yy * W + min(max(x + dx, 0), W - 1)];
+        const int yy = min(max(y + dy, 0), H - 1) - (y0 - 1);
+        for (int dx = -1; dx <= 1; ++dx) v[k++] = ss[yy][min(max(x + dx, 0), W - 1) - (x0 - 1)];
     }
     // odd-even transposition network: exact selection of the median (no arithmetic)
 #pragma unroll
@@ -1030,7 +1072,7 @@ static dim3 grid2d(int W, int H, int bx, const DevParams& P) { return dim3((W + 
 static dim3 grid1d(size_t n, const DevParams& P) { return dim3((unsigned)n, 1, P.npairs); }
 
 void launch_outlier(RefineBufs& B, const DevParams& P, hipStream_t st) {
-    hipLaunchKernelGGL(k_outlier_row, grid1d(P.H, P), dim3(256), (size_t)P.W, st, B.disp0, B.disp1, B.dm, P);
+    hipLaunchKernelGGL(k_outlier_row, grid1d(P.H, P), dim3(256), (size_t)P.W, st, B.disp0, B.disp1, B.dm, B.hist, P);
     trace_point("k_outlier", st);
 }
 
@@ -1080,33 +1122,28 @@ void launch_interpolation(RefineBufs& B, const uint32_t* img0, const DevParams& 
 
 void launch_discontinuity(RefineBufs& B, const float* vol0, const DevParams& P,
                           hipStream_t st) {
+    (void)vol0;
     const int n = P.H * P.W;
     const size_t ps = P.pstride;
-    hipLaunchKernelGGL(k_zero_u32, grid1d(1, P), dim3(256), 0, st, reinterpret_cast<uint32_t*>(B.hist), 256, ps); trace_point("k_zero_u32", st);
-    hipLaunchKernelGGL(k_gray_hist, grid1d(std::min((n + 255) / 256, 1024), P), dim3(256), 0, st, B.dm, B.gray, B.hist, n, ps); trace_point("k_gray_hist", st);
-    uint8_t* lut = reinterpret_cast<uint8_t*>(B.hist + 256);
-    hipLaunchKernelGGL(k_eq_lut, grid1d(1, P), dim3(256), 0, st, B.hist, lut, n, ps); trace_point("k_eq_lut", st);
-    hipLaunchKernelGGL(k_eq_blur, grid2d(P.W, P.H, 256, P), dim3(256), 0, st, B.gray, lut,
-                       B.gray_eq, B.blurred, P.H, P.W, ps); trace_point("k_eq_blur", st);
-    hipLaunchKernelGGL(k_sobel, grid2d(P.W, P.H, 256, P), dim3(256), 0, st, B.blurred, B.dx, B.dy, B.mag, P.H, P.W, ps); trace_point("k_sobel", st);
-    hipLaunchKernelGGL(k_nms, grid2d(P.W, P.H, 256, P), dim3(256), 0, st, B.dx, B.dy, B.mag, B.map,
-                       P.H, P.W, P.canny_low, P.canny_high, ps); trace_point("k_nms", st);
+    // the histogram was zeroed by k_outlier_row
+    hipLaunchKernelGGL(k_gray_hist, grid1d(std::min((n + 255) / 256, 1024), P), dim3(256), 0, st, B.dm, B.gray,
+                       B.hist, n, ps); trace_point("k_gray_hist", st);
+    hipLaunchKernelGGL(k_canny_front, dim3((P.W + CF_TX - 1) / CF_TX, (P.H + CF_TY - 1) / CF_TY, P.npairs), dim3(256), 0,
+                       st, B.gray, B.hist, B.gray_eq, B.map, B.strong, P.H, P.W, P.canny_low, P.canny_high, ps);
+    trace_point("k_canny_front", st);
     hipLaunchKernelGGL(k_uf_tile, dim3((P.W + UT - 1) / UT, (P.H + UT - 1) / UT, P.npairs), dim3(256), 0, st, B.map,
                        B.label, P.H, P.W, ps); trace_point("k_uf_tile", st);
     hipLaunchKernelGGL(k_uf_edges, grid2d(P.W, P.H, 256, P), dim3(256), 0, st, B.map, B.label, P.H, P.W, ps); trace_point("k_uf_edges", st);
-    hipLaunchKernelGGL(k_zero_u32, grid1d((n / 4 + 256) / 256, P), dim3(256), 0, st, reinterpret_cast<uint32_t*>(B.strong), (n + 3) / 4, ps); trace_point("k_zero_u32", st);
     hipLaunchKernelGGL(k_uf_flatten_mark, grid1d((n + 255) / 256, P), dim3(256), 0, st, B.map, B.label, B.strong, n, ps); trace_point("k_uf_flatten_mark", st);
-    hipLaunchKernelGGL(k_uf_final, grid1d((n + 255) / 256, P), dim3(256), 0, st, B.map, B.label, B.strong, B.edges, n, ps); trace_point("k_uf_final", st);
-    hipLaunchKernelGGL(k_adjust, grid2d(P.W, P.H, 256, P), dim3(256), 0, st, B.dm, B.dtmp, B.edges, vol0, P); trace_point("k_adjust", st);
-    std::swap(B.dm, B.dtmp);
 }
 
-void launch_subpixel_median(const RefineBufs& B, const float* vol0, const uint32_t* orig_left,
-                            const PairOut& outs, size_t out_step, int roi_or_mask, int offset,
-                            const DevParams& P, hipStream_t st) {
-    hipLaunchKernelGGL(k_subpix, grid2d(P.W, P.H, 256, P), dim3(256), 0, st, B.dm, vol0, B.subpix, P); trace_point("k_subpix", st);
-    hipLaunchKernelGGL(k_median_out, grid2d(P.W, P.H, 256, P), dim3(256), 0, st, B.subpix, outs,
-                       out_step, orig_left, roi_or_mask, offset, P.H, P.W, P.pstride); trace_point("k_median_out", st);
+void launch_refine_tail(RefineBufs& B, const float* vol0, const uint32_t* orig_left, const PairOut& outs,
+                        size_t out_step, int roi_or_mask, int offset, const DevParams& P, hipStream_t st) {
+    hipLaunchKernelGGL(k_refine_tail, dim3((P.W + RT_TX - 1) / RT_TX, (P.H + RT_TY - 1) / RT_TY, P.npairs), dim3(256), 0,
+                       st, B.map, B.label, B.strong, B.edges, B.dm, B.dtmp, vol0, B.subpix, outs, out_step, orig_left,
+                       roi_or_mask, offset, P);
+    trace_point("k_refine_tail", st);
+    std::swap(B.dm, B.dtmp);  // dm = the adjusted map
 }
 
 void launch_vol_to_ref(const float* vol, float* ref, int views, const DevParams& P, hipStream_t st) {

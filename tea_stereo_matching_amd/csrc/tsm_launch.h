@@ -72,12 +72,8 @@ struct RefineBufs {
     int32_t* long_list; // [H][W] indices into hv_list of the ranks with long carries
     int32_t* counts;  // [4]
     uint8_t* gray;    // [H][W]
-    int32_t* hist;    // [256] + 64 ints of LUT scratch
+    int32_t* hist;    // [256] histogram (+ 64 spare ints)
     uint8_t* gray_eq; // [H][W] equalised gray (debug dump)
-    uint8_t* blurred; // [H][W]
-    int16_t* dx;      // [H][W]
-    int16_t* dy;      // [H][W]
-    int32_t* mag;     // [H][W]
     uint8_t* map;     // [H][W]
     int32_t* label;   // [H][W]
     uint8_t* strong;  // [H][W]
@@ -98,9 +94,10 @@ void launch_interpolation(RefineBufs& B, const uint32_t* img0, const DevParams& 
                           hipStream_t st);
 void launch_discontinuity(RefineBufs& B, const float* vol0, const DevParams& P,
                           hipStream_t st);
-void launch_subpixel_median(const RefineBufs& B, const float* vol0, const uint32_t* orig_left,
-                            const PairOut& outs, size_t out_step, int roi_or_mask, int offset,
-                            const DevParams& P, hipStream_t st);
+// edge map, discontinuity adjustment, subpixel step, median + store (one launch); dm then
+// holds the adjusted map
+void launch_refine_tail(RefineBufs& B, const float* vol0, const uint32_t* orig_left, const PairOut& outs,
+                        size_t out_step, int roi_or_mask, int offset, const DevParams& P, hipStream_t st);
 
 // debug helpers (pair 0 of the group)
 void launch_vol_to_ref(const float* vol, float* ref, int views, const DevParams& P,
