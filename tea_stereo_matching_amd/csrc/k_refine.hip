@@ -554,83 +554,93 @@ __constant__ int c_ray_w[16] = {0, 2, 2, 2, 0, -2, -2, -2, 1, 2, 2, 1, -1, -2, -
 // the reference's two post-loops (:1211-1216 min for occlusions, :1222-1231 colour-diff
 // selection for mismatches): no per-thread arrays, no dynamic register indexing.
 
-// Ray-parallel form: 16 lanes per pixel, lane = ray, 4 pixels of a row per wave.  The
-// rays' dependent load chains (<= max_search_depth steps each) run side by side instead
-// of one after another; the per-ray results are then folded in ray order exactly as
-// above (a min for occlusions, the colour-difference rule for mismatches).
+// Ray-parallel form: 16 lanes per pixel, lane = ray, 4 pixels a wave.  The rays' dependent
+// load chains (<= max_search_depth steps each) run side by side instead of one after
+// another; the per-ray results are then folded in ray order exactly as above (a min for
+// occlusions, the colour-difference rule for mismatches).
+// Over the last voting pass's ranked outliers only (round 6; grid-stride over the ranks): the
+// Jacobi output dtmp already equals the map everywhere else -- k_vote_prep copied the pass's
+// input into it and the decision changed only ranked outliers -- so a ranked pixel that the
+// decision made valid is copied, an outlier is interpolated, and nothing else is touched
+// (one pixel group a rank instead of a 16-lane group for every pixel of the image).
 __global__ __launch_bounds__(256) void k_interp_rays(const int32_t* __restrict__ disp, int32_t* __restrict__ out,
-                                                     const uint32_t* __restrict__ img0, DevParams Pk) {
+                                                     const uint32_t* __restrict__ img0,
+                                                     const int32_t* __restrict__ out_list,
+                                                     const int32_t* __restrict__ counts, DevParams Pk) {
     const DevParams P = Pk;
-    pair_shift(blockIdx.z, P.pstride, disp, out, img0);
+    pair_shift(blockIdx.z, P.pstride, disp, out, img0, out_list, counts);
     const int lane = threadIdx.x & 63;
     const int dir = lane & 15;
-    const int x = (blockIdx.x * blockDim.x + threadIdx.x) >> 4;  // 16 lanes per pixel
-    const int y = blockIdx.y;
     const int H = P.H, W = P.W, minD = P.minD;
-    const bool inside = x < W;
-    const size_t idx = (size_t)y * W + (inside ? x : W - 1);
-    const int cur = disp[idx];
-    const bool outlier = inside && cur < minD;
-    if (!__any(outlier)) {  // the whole wave: no outlier
-        if (inside && dir == 0) out[idx] = cur;
-        return;
-    }
-    int nd = cur, ndiff = -1;
-    if (outlier) {
-        const uint32_t c0 = img0[idx];
-        const int rh = c_ray_h[dir], rw = c_ray_w[dir];
-        const int sh0 = rh / 2, sh1 = rh - rh / 2, sw0 = rw / 2, sw1 = rw - rw / 2;
-        // RI_B steps a round trip: their positions, then their loads back to back, then the
-        // first in-image valid one in step order (a ray moves monotonically, so it never
-        // re-enters the image once it has left it)
-        int hD = y, wD = x;
-        bool done = false;
-        for (int s0 = 0; s0 < P.max_search_depth && !done; s0 += RI_B) {
-            size_t at[RI_B];
-            bool ok[RI_B];
-            int dv[RI_B];
+    const int nout = counts[0];
+    const int ngroups = (gridDim.x * blockDim.x) >> 4;
+    // every group of a wave runs the same number of iterations (shuffles stay in step)
+    const int g0 = (blockIdx.x * blockDim.x + threadIdx.x) >> 4;
+    for (int it = g0 & ~3; it < nout; it += ngroups) {
+        const int a = it + (g0 & 3);
+        const bool inside = a < nout;
+        const int p = inside ? out_list[a] : out_list[nout - 1];
+        const int y = p / W, x = p - y * W;
+        const size_t idx = (size_t)p;
+        const int cur = disp[idx];
+        const bool outlier = inside && cur < minD;
+        int nd = cur, ndiff = -1;
+        if (outlier) {
+            const uint32_t c0 = img0[idx];
+            const int rh = c_ray_h[dir], rw = c_ray_w[dir];
+            const int sh0 = rh / 2, sh1 = rh - rh / 2, sw0 = rw / 2, sw1 = rw - rw / 2;
+            // RI_B steps a round trip: their positions, then their loads back to back, then the
+            // first in-image valid one in step order (a ray moves monotonically, so it never
+            // re-enters the image once it has left it)
+            int hD = y, wD = x;
+            bool done = false;
+            for (int s0 = 0; s0 < P.max_search_depth && !done; s0 += RI_B) {
+                size_t at[RI_B];
+                bool ok[RI_B];
+                int dv[RI_B];
 #pragma unroll
-            for (int k = 0; k < RI_B; ++k) {
-                const int s = s0 + k;
-                hD += (s & 1) ? sh1 : sh0;
-                wD += (s & 1) ? sw1 : sw0;
-                ok[k] = s < P.max_search_depth && hD >= 0 && hD < H && wD >= 0 && wD < W;
-                at[k] = ok[k] ? (size_t)hD * W + wD : idx;
-            }
+                for (int k = 0; k < RI_B; ++k) {
+                    const int s = s0 + k;
+                    hD += (s & 1) ? sh1 : sh0;
+                    wD += (s & 1) ? sw1 : sw0;
+                    ok[k] = s < P.max_search_depth && hD >= 0 && hD < H && wD >= 0 && wD < W;
+                    at[k] = ok[k] ? (size_t)hD * W + wD : idx;
+                }
 #pragma unroll
-            for (int k = 0; k < RI_B; ++k) dv[k] = ok[k] ? disp[at[k]] : 0;
+                for (int k = 0; k < RI_B; ++k) dv[k] = ok[k] ? disp[at[k]] : 0;
 #pragma unroll
-            for (int k = 0; k < RI_B; ++k) {
-                if (done) break;
-                if (!ok[k]) { done = true; break; }
-                if (dv[k] >= minD) {
-                    nd = dv[k];
-                    ndiff = color_diff(P, c0, img0[at[k]]);
-                    done = true;
+                for (int k = 0; k < RI_B; ++k) {
+                    if (done) break;
+                    if (!ok[k]) { done = true; break; }
+                    if (dv[k] >= minD) {
+                        nd = dv[k];
+                        ndiff = color_diff(P, c0, img0[at[k]]);
+                        done = true;
+                    }
                 }
             }
         }
-    }
-    // fold the 16 rays of this lane's pixel in ray order (every lane of the group
-    // computes the same result; lane dir == 0 writes it)
-    const int base = lane & ~15;
-    const bool occlusion = cur == minD - 1;  // :1209
-    int res = 0, mdiff = -1;
+        // fold the 16 rays of this lane's pixel in ray order (every lane of the group
+        // computes the same result; lane dir == 0 writes it)
+        const int base = lane & ~15;
+        const bool occlusion = cur == minD - 1;  // :1209
+        int res = 0, mdiff = -1;
 #pragma unroll
-    for (int d = 0; d < 16; ++d) {
-        const int n_d = __shfl(nd, base + d);
-        const int f_d = __shfl(ndiff, base + d);
-        if (occlusion) {
-            res = d == 0 ? n_d : min(res, n_d);
-        } else if (d == 0) {
-            res = n_d;
-            mdiff = f_d;
-        } else if (mdiff < 0 || (mdiff > f_d && f_d > 0)) {
-            res = n_d;
-            mdiff = f_d;
+        for (int d = 0; d < 16; ++d) {
+            const int n_d = __shfl(nd, base + d);
+            const int f_d = __shfl(ndiff, base + d);
+            if (occlusion) {
+                res = d == 0 ? n_d : min(res, n_d);
+            } else if (d == 0) {
+                res = n_d;
+                mdiff = f_d;
+            } else if (mdiff < 0 || (mdiff > f_d && f_d > 0)) {
+                res = n_d;
+                mdiff = f_d;
+            }
         }
+        if (inside && dir == 0) out[idx] = outlier ? res : cur;
     }
-    if (inside && dir == 0) out[idx] = outlier ? res : cur;
 }
 
 // ---------------------------------------------------------------------------
@@ -1115,7 +1125,9 @@ void launch_region_voting(RefineBufs& B, const uint32_t* arms0, int hf, const De
 
 void launch_interpolation(RefineBufs& B, const uint32_t* img0, const DevParams& P,
                           hipStream_t st) {
-    hipLaunchKernelGGL(k_interp_rays, grid2d(P.W * 16, P.H, 256, P), dim3(256), 0, st, B.dm, B.dtmp, img0, P);
+    // the ranked outliers of the last voting pass (out_list, counts[0]): dtmp equals dm elsewhere
+    const int ib = std::max(64, 2048 / std::max(1, P.npairs));
+    hipLaunchKernelGGL(k_interp_rays, grid1d(ib, P), dim3(256), 0, st, B.dm, B.dtmp, img0, B.out_list, B.counts, P);
     trace_point("k_interp", st);
     std::swap(B.dm, B.dtmp);
 }
