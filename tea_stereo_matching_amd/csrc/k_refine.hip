@@ -221,7 +221,7 @@ __global__ __launch_bounds__(SC_THREADS) void k_vote_prep(const int32_t* __restr
     if (threadIdx.x == SC_THREADS - 1 && (int)blockIdx.x == nb - 1) {
         counts[0] = first + total;
         counts[1] = 0;
-        counts[2] = 0;  // the decision's long-carry list (k_vote_decide_wave)
+        counts[2] = 0;  // the long-carry list (k_hv_list)
         rank[n] = first + total;
     }
     {
@@ -334,33 +334,96 @@ __global__ __launch_bounds__(256) void k_vote_count_rank(const int32_t* __restri
     }
 }
 
+
+constexpr int VD_WAVES = 4;
+constexpr int VD_CB = 8;      // carried votes loaded a lane per round trip (512 ranks a wave)
+constexpr int VD_LONG = 512;  // carries longer than this are decided by a workgroup a rank
+constexpr int VL_BLOCKS = 64; // the decision launch's long-carry workgroups
+
 // The high-vote outliers (vote > votingThresh, :1132) listed in rank order: hv_list[k] = the
 // rank of the k-th one, counts[1] = how many.  One single-pass launch over the ranks, as the
-// outlier ranking (k_vote_prep): its own flags after the ranking's nb.
+// outlier ranking (k_vote_prep): its own flags after the ranking's nb.  It also lists the
+// high-vote ranks whose carry is longer than VD_LONG ranks (long_list[i] = k, counts[2] = how
+// many, zeroed by k_vote_prep), which the decision launch's long-carry workgroups take while
+// its waves take the rest: a rank is long when no high-vote rank lies in the VD_LONG + 1 ranks
+// before it -- the previous one inside the block from a max-scan of the threads' last
+// high-vote ranks, before the block from one search of the block's threads over that window,
+// issued before the wait for the preceding blocks' counts (its latency hides behind it).
 __global__ __launch_bounds__(SC_THREADS) void k_hv_list(const int32_t* __restrict__ cvote, int32_t* __restrict__ counts,
                                                         uint64_t* __restrict__ flags, int32_t* __restrict__ hv_list,
-                                                        int thresh, uint32_t epoch, size_t ps) {
-    pair_shift(blockIdx.z, ps, cvote, counts, flags, hv_list);
-    __shared__ int sa[SC_THREADS], sb[SC_THREADS];
-    __shared__ int s_base;
-    if (threadIdx.x == 0) s_base = 0;
+                                                        int32_t* __restrict__ long_list, int thresh, uint32_t epoch,
+                                                        size_t ps) {
+    pair_shift(blockIdx.z, ps, cvote, counts, flags, hv_list, long_list);
+    constexpr int NW = SC_THREADS / 64;
+    __shared__ int s_sum[NW], s_last[NW], s_first[NW];
+    __shared__ int s_base, s_found;
+    const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
+    if (t == 0) { s_base = 0; s_found = -1; }
     const int nout = counts[0];
-    const int base = blockIdx.x * SC_BLOCK + threadIdx.x * SC_ITEMS;
+    const int base = blockIdx.x * SC_BLOCK + t * SC_ITEMS;
     int f[SC_ITEMS];
-    int a = 0, b = 0;
+    int a = 0, mylast = -1, myfirst = 0x7fffffff;
 #pragma unroll
     for (int k = 0; k < SC_ITEMS; ++k) {
         f[k] = base + k < nout && cvote[base + k] > thresh ? 1 : 0;
         a += f[k];
+        if (f[k]) {
+            mylast = base + k;
+            myfirst = min(myfirst, base + k);
+        }
     }
-    block_scan2(a, b, sa, sb);  // its barriers also publish s_base = 0
-    const int total = sa[SC_THREADS - 1];
+    // per wave: inclusive sums of the counts, inclusive max of the last ranks, min of the first
+    int isum = a, ilast = mylast, fmin = myfirst;
+#pragma unroll
+    for (int off = 1; off < 64; off <<= 1) {
+        const int vs = __shfl_up(isum, off), vl = __shfl_up(ilast, off);
+        if (lane >= off) { isum += vs; ilast = max(ilast, vl); }
+        fmin = min(fmin, __shfl_xor(fmin, off));
+    }
+    if (lane == 63) { s_sum[wv] = isum; s_last[wv] = ilast; s_first[wv] = fmin; }
+    __syncthreads();
+    int excl = isum - a, prev = __shfl_up(ilast, 1), total = 0, r0 = 0x7fffffff;
+    if (lane == 0) prev = -1;
+#pragma unroll
+    for (int w = 0; w < NW; ++w) {
+        if (w < wv) { excl += s_sum[w]; prev = max(prev, s_last[w]); }
+        total += s_sum[w];
+        r0 = min(r0, s_first[w]);
+    }
+    // before the block: the nearest high-vote rank among the VD_LONG + 1 ranks before r0, the
+    // block's first one (loads issued now, used after the wait below)
+    const int bbase = blockIdx.x * SC_BLOCK;
+    const bool search = total > 0 && bbase > 0 && r0 - bbase <= VD_LONG;  // block-uniform
+    const int lo = max(0, r0 - VD_LONG - 1);
+    // (the window is at most VD_LONG + 1 = 513 ranks: two loads a thread and one more)
+    static_assert(VD_LONG + 1 <= 2 * SC_THREADS + 1, "the search window's loads");
+    int c0 = 0, c1 = 0, c2 = 0;
+    const int q0 = bbase - 1 - t, q1 = q0 - SC_THREADS, q2 = bbase - 1 - 2 * SC_THREADS;
+    if (search) {
+        c0 = q0 >= lo ? cvote[q0] : 0;
+        c1 = q1 >= lo ? cvote[q1] : 0;
+        c2 = t == 0 && q2 >= lo ? cvote[q2] : 0;
+    }
     const int first = block_exclusive(flags + gridDim.x, blockIdx.x, epoch, total, &s_base);
-    a += first;
-    if (threadIdx.x == SC_THREADS - 1 && blockIdx.x == gridDim.x - 1) counts[1] = first + total;
+    if (t == SC_THREADS - 1 && blockIdx.x == gridDim.x - 1) counts[1] = first + total;
+    int pos = first + excl;  // this thread's first list position
+    if (total == 0) return;  // block-uniform
+    if (search) {
+        const int found = c0 > thresh ? q0 : (c1 > thresh ? q1 : (c2 > thresh ? q2 : -1));
+        if (found >= 0) atomicMax(&s_found, found);
+        __syncthreads();
+    }
+    if (prev < 0) prev = s_found;
 #pragma unroll
     for (int k = 0; k < SC_ITEMS; ++k)
-        if (f[k]) hv_list[a++] = base + k;
+        if (f[k]) {
+            const int r = base + k;
+            hv_list[pos] = r;
+            // a rank's carry: the ranks strictly between the previous high-vote rank and it
+            if (r - prev - 1 > VD_LONG) long_list[atomicAdd(&counts[2], 1)] = pos;
+            prev = r;
+            ++pos;
+        }
 }
 
 // The decision, one wave per high-vote outlier r_k (grid-stride over k): its own region into a
@@ -368,28 +431,37 @@ __global__ __launch_bounds__(SC_THREADS) void k_hv_list(const int32_t* __restric
 // previous high-vote one r_{k-1} and r_k -- exactly the histogram the reference carries in
 // raster order (:1132-1151: hist is cleared only by a high-vote decision) -- then the first
 // argmax and the ratio test (:1137-1153).  No workgroup barrier: every wave is independent.
-constexpr int VD_WAVES = 4;
-constexpr int VD_CB = 8;      // carried votes loaded a lane per round trip (512 ranks a wave)
-constexpr int VD_LONG = 512;  // carries longer than this go to k_vote_decide_long (a workgroup a rank)
-__global__ __launch_bounds__(VD_WAVES * 64) void k_vote_decide_wave(
+// One launch: workgroups [0, VL_BLOCKS) take the long carries listed by k_hv_list (a
+// workgroup a rank, below), the others the rest (a wave a rank), side by side.
+template <int NT>
+__device__ void vote_decide_long(const int32_t* __restrict__ disp, int32_t* __restrict__ dtmp,
+                                 const uint32_t* __restrict__ arms, const int32_t* __restrict__ out_list,
+                                 const int32_t* __restrict__ cvote, const uint16_t* __restrict__ csamp,
+                                 const int32_t* __restrict__ counts, const int32_t* __restrict__ hv_list,
+                                 const int32_t* __restrict__ long_list, int hf, const DevParams& P, int* hist);
+
+__global__ __launch_bounds__(VD_WAVES * 64) void k_vote_decide(
     const int32_t* __restrict__ disp, int32_t* __restrict__ dtmp, const uint32_t* __restrict__ arms,
     const int32_t* __restrict__ out_list, const int32_t* __restrict__ cvote, const uint16_t* __restrict__ csamp,
-    int32_t* __restrict__ counts, const int32_t* __restrict__ hv_list, int32_t* __restrict__ long_list, int hf,
-    DevParams Pk) {
+    const int32_t* __restrict__ counts, const int32_t* __restrict__ hv_list, const int32_t* __restrict__ long_list,
+    int hf, DevParams Pk) {
     const DevParams P = Pk;
     pair_shift(blockIdx.z, P.pstride, disp, dtmp, arms, out_list, cvote, csamp, counts, hv_list, long_list);
     extern __shared__ int hist[];
+    if ((int)blockIdx.x < VL_BLOCKS) {
+        vote_decide_long<VD_WAVES * 64>(disp, dtmp, arms, out_list, cvote, csamp, counts, hv_list, long_list, hf, P,
+                                        hist);
+        return;
+    }
     const int L = P.L, W = P.W, minD = P.minD;
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
     int* h = hist + wv * L;
     const int nhv = counts[1];
-    for (int k = blockIdx.x * VD_WAVES + wv; k < nhv; k += gridDim.x * VD_WAVES) {
+    const int bx = (int)blockIdx.x - VL_BLOCKS, gx = (int)gridDim.x - VL_BLOCKS;
+    for (int k = bx * VD_WAVES + wv; k < nhv; k += gx * VD_WAVES) {
         const int r = hv_list[k];
         const int prev = k > 0 ? hv_list[k - 1] : -1;
-        if (r - prev - 1 > VD_LONG) {  // a long carry: a whole workgroup takes it (next launch)
-            if (lane == 0) long_list[atomicAdd(&counts[2], 1)] = k;
-            continue;
-        }
+        if (r - prev - 1 > VD_LONG) continue;  // a long carry: one of the long-carry workgroups
         for (int d = lane; d < L; d += 64) h[d] = 0;
         wave_lds_sync();  // the zeroed bins before any lane's atomics (lanes share the histogram)
         const int p = out_list[r];
@@ -465,21 +537,19 @@ __global__ __launch_bounds__(VD_WAVES * 64) void k_vote_decide_wave(
 }
 
 // The high-vote outliers whose carry is longer than VD_LONG ranks (synthetic scenes: a few
-// per pass, carrying thousands of low-vote outliers), a workgroup each: the region split over
+// per pass, carrying thousands of low-vote outliers), a workgroup of NT threads each: the region split over
 // its threads by outer position, the carry over all its threads, then the same decision.
-constexpr int VL_THREADS = 512;
-__global__ __launch_bounds__(VL_THREADS) void k_vote_decide_long(
-    const int32_t* __restrict__ disp, int32_t* __restrict__ dtmp, const uint32_t* __restrict__ arms,
-    const int32_t* __restrict__ out_list, const int32_t* __restrict__ cvote, const uint16_t* __restrict__ csamp,
-    const int32_t* __restrict__ counts, const int32_t* __restrict__ hv_list, const int32_t* __restrict__ long_list,
-    int hf, DevParams Pk) {
-    const DevParams P = Pk;
-    pair_shift(blockIdx.z, P.pstride, disp, dtmp, arms, out_list, cvote, csamp, counts, hv_list, long_list);
-    extern __shared__ int hist[];
+template <int NT>
+__device__ void vote_decide_long(const int32_t* __restrict__ disp, int32_t* __restrict__ dtmp,
+                                 const uint32_t* __restrict__ arms, const int32_t* __restrict__ out_list,
+                                 const int32_t* __restrict__ cvote, const uint16_t* __restrict__ csamp,
+                                 const int32_t* __restrict__ counts, const int32_t* __restrict__ hv_list,
+                                 const int32_t* __restrict__ long_list, int hf, const DevParams& P, int* hist) {
+    constexpr int VL_THREADS = NT;
     const int L = P.L, W = P.W, minD = P.minD;
     const int tid = threadIdx.x, lane = tid & 63;
     const int nlong = counts[2];
-    for (int i = blockIdx.x; i < nlong; i += gridDim.x) {
+    for (int i = blockIdx.x; i < nlong; i += VL_BLOCKS) {
         const int k = long_list[i];
         const int r = hv_list[k];
         const int prev = k > 0 ? hv_list[k - 1] : -1;
@@ -1106,20 +1176,18 @@ void launch_region_voting(RefineBufs& B, const uint32_t* arms0, int hf, const De
                        B.counts, B.cvote, B.csamp, B.vpre, hf, P);
     trace_point("k_vote_count_rank", st);
     hipLaunchKernelGGL(k_hv_list, grid1d(nb, P), dim3(SC_THREADS), 0, st, B.cvote, B.counts, B.flags, B.hv_list,
-                       P.voting_thresh, ep, ps);
+                       B.long_list, P.voting_thresh, ep, ps);
     trace_point("k_hv_list", st);
-    // one wave per high-vote outlier, grid-stride; a histogram of L ints per wave
+    // one wave per high-vote outlier, grid-stride; a histogram of L ints per wave; the first
+    // VL_BLOCKS workgroups take the long carries (one histogram of L ints)
     const size_t lds = (size_t)VD_WAVES * P.L * sizeof(int);
     static_assert((size_t)VD_WAVES * 2048 * sizeof(int) <= 64 * 1024, "vote-decision LDS past the default limit");
     // a wave a high-vote rank where the list is long (real pairs: tens of thousands): 16384
     // blocks measured 110 against 121 us a launch on the 0600 pair (4096), config B unchanged
     const int vd_blocks = std::max(64, 16384 / std::max(1, P.npairs));
-    hipLaunchKernelGGL(k_vote_decide_wave, grid1d(vd_blocks, P), dim3(VD_WAVES * 64), lds, st, B.dm, B.dtmp, arms0,
-                       B.out_list, B.cvote, B.csamp, B.counts, B.hv_list, B.long_list, hf, P);
-    trace_point("k_vote_decide_wave", st);
-    hipLaunchKernelGGL(k_vote_decide_long, grid1d(64, P), dim3(VL_THREADS), (size_t)P.L * sizeof(int), st, B.dm,
-                       B.dtmp, arms0, B.out_list, B.cvote, B.csamp, B.counts, B.hv_list, B.long_list, hf, P);
-    trace_point("k_vote_decide_long", st);
+    hipLaunchKernelGGL(k_vote_decide, grid1d(VL_BLOCKS + vd_blocks, P), dim3(VD_WAVES * 64), lds, st, B.dm, B.dtmp,
+                       arms0, B.out_list, B.cvote, B.csamp, B.counts, B.hv_list, B.long_list, hf, P);
+    trace_point("k_vote_decide", st);
     std::swap(B.dm, B.dtmp);
 }
 

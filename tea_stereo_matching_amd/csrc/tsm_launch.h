@@ -69,7 +69,7 @@ struct RefineBufs {
     uint16_t* csamp;  // [H][W][20] low-vote samples by outlier rank
     uint64_t* flags;  // single-pass scan flags (epoch << 32 | count), refine_flag_words
     int32_t* hv_list; // [H][W] ranks of the high-vote outliers of a voting pass, in rank order
-    int32_t* long_list; // [H][W] indices into hv_list of the ranks with long carries
+    int32_t* long_list; // [H][W] list positions of the high-vote ranks with long carries
     int32_t* counts;  // [4]
     uint8_t* gray;    // [H][W]
     int32_t* hist;    // [256] histogram (+ 64 spare ints)
