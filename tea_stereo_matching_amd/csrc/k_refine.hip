@@ -722,7 +722,10 @@ __global__ __launch_bounds__(256) void k_interp_rays(const int32_t* __restrict__
 // ---------------------------------------------------------------------------
 // gray = (uchar)max(d, 0) (:1249, wraps > 255) and its histogram (the LUT is built by every
 // block of k_canny_front from it: a last-block LUT here needed a device-scope fence in every
-// block, which wrote the gray bytes back out of L2 -- 67 against 15 us, round 6)
+// block, which wrote the gray bytes back out of L2 -- 67 against 15 us, round 6).  A thread
+// takes 16 consecutive pixels (16-B loads and one 16-B store) and adds each run of equal
+// values to the block's histogram once: a disparity map is piecewise constant, and one LDS
+// atomic per pixel serialised on the few busy bins.
 __global__ __launch_bounds__(256) void k_gray_hist(const int32_t* __restrict__ disp, uint8_t* __restrict__ gray,
                                                    int32_t* __restrict__ hist, int n, size_t ps) {
     pair_shift(blockIdx.z, ps, disp, gray, hist);
@@ -730,11 +733,30 @@ __global__ __launch_bounds__(256) void k_gray_hist(const int32_t* __restrict__ d
     const int k = threadIdx.x;
     h[k] = 0;
     __syncthreads();
-    for (int i = blockIdx.x * blockDim.x + k; i < n; i += gridDim.x * blockDim.x) {
-        const int d = disp[i];
-        const uint8_t g = d < 0 ? 0 : (uint8_t)d;  // (uchar) wraps > 255 (:1249)
-        gray[i] = g;
-        atomicAdd(&h[g], 1);
+    const int base = (blockIdx.x * 256 + k) * SC_ITEMS;
+    if (base < n) {
+        int dv[SC_ITEMS];
+        load_items(disp, base, n, dv);  // past n: INT_MAX
+        uint8_t g[SC_ITEMS];
+#pragma unroll
+        for (int i = 0; i < SC_ITEMS; ++i) g[i] = dv[i] < 0 ? 0 : (uint8_t)dv[i];  // (uchar) wraps > 255 (:1249)
+        int run = 0;
+        for (int i = 0; i < SC_ITEMS && base + i < n; ++i) {
+            ++run;
+            if (i + 1 == SC_ITEMS || base + i + 1 >= n || g[i + 1] != g[i]) {
+                atomicAdd(&h[g[i]], run);
+                run = 0;
+            }
+        }
+        if (base + SC_ITEMS <= n) {
+            uint32_t w[4];
+#pragma unroll
+            for (int q = 0; q < 4; ++q)
+                w[q] = g[4 * q] | (g[4 * q + 1] << 8) | (g[4 * q + 2] << 16) | ((uint32_t)g[4 * q + 3] << 24);
+            *reinterpret_cast<uint4*>(gray + base) = make_uint4(w[0], w[1], w[2], w[3]);
+        } else {
+            for (int i = 0; i < SC_ITEMS && base + i < n; ++i) gray[base + i] = g[i];
+        }
     }
     __syncthreads();
     if (h[k]) atomicAdd(&hist[k], h[k]);
@@ -1206,8 +1228,8 @@ void launch_discontinuity(RefineBufs& B, const float* vol0, const DevParams& P,
     const int n = P.H * P.W;
     const size_t ps = P.pstride;
     // the histogram was zeroed by k_outlier_row
-    hipLaunchKernelGGL(k_gray_hist, grid1d(std::min((n + 255) / 256, 1024), P), dim3(256), 0, st, B.dm, B.gray,
-                       B.hist, n, ps); trace_point("k_gray_hist", st);
+    hipLaunchKernelGGL(k_gray_hist, grid1d((n + 256 * SC_ITEMS - 1) / (256 * SC_ITEMS), P), dim3(256), 0, st, B.dm,
+                       B.gray, B.hist, n, ps); trace_point("k_gray_hist", st);
     hipLaunchKernelGGL(k_canny_front, dim3((P.W + CF_TX - 1) / CF_TX, (P.H + CF_TY - 1) / CF_TY, P.npairs), dim3(256), 0,
                        st, B.gray, B.hist, B.gray_eq, B.map, B.strong, P.H, P.W, P.canny_low, P.canny_high, ps);
     trace_point("k_canny_front", st);
