@@ -129,6 +129,9 @@ SCAN_CASES = [
     (48, 20, 300, 0, 240, 0, False, False),
     (6, 40, 96, 0, 48, 0, True, False),   # ROI / mask: maxD = W/2 (:339-340)
     (7, 40, 96, 0, 48, 1, False, True),
+    # very wide rows (the horizontal passes' longest walks, the widest colour-difference rows)
+    (52, 5, 4000, 0, 30, 0, False, False),
+    (51, 3, 20600, 0, 16, 0, False, False),
 ]
 
 
