@@ -156,7 +156,27 @@ static void run(const char* name, float* vol, int H, int W, int Lp, int reps, fl
     hipEventDestroy(b);
 }
 
+// placement: time the same walk in a series of large allocations kept alive side by side
+static int placement(int nbuf, size_t gb) {
+    const int H = 720, W = 1280;
+    const size_t vol = (size_t)2 * H * W * 196 * 4;
+    float* bufs[16] = {};
+    for (int i = 0; i < nbuf && i < 16; ++i) {
+        if (hipMalloc(&bufs[i], gb << 30) != hipSuccess) { printf("alloc %d failed\n", i); return 1; }
+        hipMemset(bufs[i], 0, gb << 30);
+        char name[64];
+        for (size_t off = 0; off + vol <= (gb << 30); off += (gb << 30) / 3) {
+            snprintf(name, sizeof name, "buf %d (%zu GB) at +%zu MB: V walk", i, gb, off >> 20);
+            run<8, 1, true, true, true>(name, bufs[i] + off / 4, H, W, 196, 5, bufs[i]);
+        }
+        fflush(stdout);
+    }
+    for (int i = 0; i < nbuf && i < 16; ++i) hipFree(bufs[i]);
+    return 0;
+}
+
 int main(int argc, char** argv) {
+    if (argc > 1 && argv[1][0] == 'p') return placement(argc > 2 ? atoi(argv[2]) : 5, argc > 3 ? atoi(argv[3]) : 20);
     const int H = argc > 2 ? atoi(argv[1]) : 720, W = argc > 2 ? atoi(argv[2]) : 1280;  // default: the 0600 pair
     float* vol = nullptr;
     float* out = nullptr;
