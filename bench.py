@@ -265,6 +265,28 @@ def main():
         verify["how"] += "; rank 0's gathered maps == every rank's (SHA-256)"
     verified = Dd.min_over_ranks(1.0 if verify["ok"] else 0.0, world, dev) == 1.0
 
+    # untimed for `value`: the same batch on a second handle of this process (same settings).
+    # Handles differ by where their two group arenas land in HBM -- 394-427 pairs/s on one box
+    # (profiles/r06_handle_spread.txt) -- so the line shows a second placement beside the
+    # headline's first-handle one.
+    m2 = tsm.ADCensus(local)
+    m2.setMatchingStrategy(tsm.ColorModel.RGB, False, False)
+    m2.setMinMaxDisparity(0, D)
+    m2.setConcurrency(args.concurrency)
+    m2.compute_batch_device_ptr(lp, rp, H, W, W * 3, op_b[0], W * 4)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t2 = time.perf_counter()
+    for _ in range(prof_steps):
+        m2.compute_batch_device_ptr(lp, rp, H, W, W * 3, op_b[0], W * 4)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    el_h2 = Dd.max_over_ranks(time.perf_counter() - t2, world, dev)
+    m2.close()
+    del m2
+
     # Host-buffer leg (untimed for `value`): the same batch handed over as host (pageable
     # numpy) images and returned to host arrays, i.e. the C ABI's tsm_adc_compute_batch with
     # its H2D / D2H copies -- the PCIe-inclusive rate of the drop-in boundary.
@@ -418,6 +440,8 @@ def main():
         "repeat_with_stage_events": {"steps": prof_steps, "pairs_per_s": round(bp * prof_steps / el_prof, 3)},
         "repeat_without": {"steps": prof_steps, "pairs_per_s": round(bp * prof_steps / el_rep, 3),
                            "step_ms_min_median_max": ms3(step_rep)},
+        "second_handle": {"steps": prof_steps, "pairs_per_s": round(bp * prof_steps / el_h2, 3),
+                          "note": "the same batch on a second handle of the process (other arena placement)"},
     }
     # the driver keeps only the line's last ~2000 characters: the bulky blocks go first and
     # a compact summary of the headline's breakdown and the real-pair stages goes last

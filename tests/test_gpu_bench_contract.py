@@ -43,4 +43,5 @@ def test_bench_json_line_small_batch():
     t = d["timed_region"]
     assert t["stage_events"] is False and len(t["step_ms_min_median_max"]) == 3
     assert t["repeat_with_stage_events"]["pairs_per_s"] > 0 and t["repeat_without"]["pairs_per_s"] > 0
+    assert t["second_handle"]["pairs_per_s"] > 0
     assert list(d)[-1] == "summary"
